@@ -1,0 +1,643 @@
+// adlsm-tree_amd/csrc/bloom_build.hip -- MI355X (gfx950) bloom-filter build.
+//
+// Replaces BloomFilter::Keys2Block (reference src/filter_block.cpp:9-33): for
+// every key, h1/h2 = murmur3 with two seeds, then k bits (h1 + j*h2) % m are
+// ORed into an (n*bpk+7)-byte bitmap.  The result is an order-independent OR,
+// so any decomposition gives the reference's bitmap bit for bit.
+//
+// Design (DESIGN.md "Build kernels"): random single-bit RMW into a 100 MB
+// bitmap cannot go through device-scope global atomics (they execute at the
+// memory side at ~20 G lanes/s chip-wide, ~3 ms for 60 M bit-sets), so the
+// bit-sets are routed through LDS in two passes:
+//
+//   pass A  bloom_bin_kernel   one workgroup per chunk of C keys: coalesced
+//           key loads, both hashes, k positions per key, an LDS counting sort
+//           of the chunk's k*C positions by bitmap tile, one coalesced write of
+//           the sorted chunk to its workspace region and of the per-tile start
+//           offsets to the (tile, chunk) table.
+//   pass B  bloom_tile_kernel  one workgroup per bitmap tile of 2^TL bits held
+//           in LDS: gathers that tile's segment from every chunk region,
+//           ds_or_b32 of every position into LDS, then one coalesced write of
+//           the finished tile.  Every bitmap byte is written exactly once, so
+//           the bitmap needs no zero-fill.
+//
+// A direct device-scope atomicOr kernel (bloom_atomic_kernel) is kept as the
+// alternative for small filters and as an independent cross-check.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <mutex>
+#include <vector>
+
+#include "bloom_common.hpp"
+
+using namespace adl_dev;
+
+namespace {
+
+constexpr int kBlockA = 1024;       // pass A threads per workgroup (16 waves)
+constexpr int kKptMax = 8;          // keys per thread, pass A
+constexpr int kBlockB = 1024;       // pass B threads per workgroup
+constexpr int kUnrollB = 8;         // gathered positions in flight per lane, pass B
+constexpr int kMaxFilters = 8;      // filters per launch pair (descriptors ride in kernargs)
+constexpr uint32_t kHistMax = 2049; // tiles per filter + 1 (m < 2^31, TL >= ... keeps T <= 2048)
+constexpr uint32_t kPosLdsWords = 36864;  // 144 KiB of sorted positions per chunk
+constexpr uint32_t kMinTileLog2 = 10;
+constexpr uint32_t kMaxTileLog2 = 20;     // 128 KiB LDS tile
+constexpr uint32_t kTargetWorkgroups = 512;
+
+struct FilterDesc {
+  uint64_t key_begin;   // first key (index into the key set)
+  uint64_t pos_base;    // u32-word offset of this filter's chunk-0 region
+  uint64_t table_base;  // u32-word offset of this filter's (tile, chunk) table
+  uint64_t bitmap_off;  // output byte offset
+  uint32_t n;           // keys
+  uint32_t alloc_bytes; // bitmap bytes rounded up to 16
+  uint32_t chunk_base;  // first pass-A workgroup
+  uint32_t tile_base;   // first pass-B workgroup
+  uint32_t chunks;      // W
+  uint32_t tiles;       // T
+  FastMod mod;          // m = 8 * bitmap bytes
+};
+
+struct BuildArgs {
+  uint32_t nf;     // filters in this launch
+  uint32_t k;      // probes per key
+  uint32_t C;      // keys per chunk
+  uint32_t TL;     // log2 tile bits
+  FilterDesc f[kMaxFilters];
+};
+
+__device__ __forceinline__ int find_filter_by_chunk(const BuildArgs &a, uint32_t wg) {
+  int f = 0;
+#pragma unroll
+  for (int i = 1; i < kMaxFilters; ++i)
+    if ((uint32_t)i < a.nf && wg >= a.f[i].chunk_base) f = i;
+  return f;
+}
+
+__device__ __forceinline__ int find_filter_by_tile(const BuildArgs &a, uint32_t wg) {
+  int f = 0;
+#pragma unroll
+  for (int i = 1; i < kMaxFilters; ++i)
+    if ((uint32_t)i < a.nf && wg >= a.f[i].tile_base) f = i;
+  return f;
+}
+
+// ---------------------------------------------------------------- pass A
+// KFIX > 0: k known at compile time, positions kept in registers between the
+// count and the scatter; KFIX == 0: runtime k, positions recomputed.
+template <int KFIX, class Keys>
+__global__ __launch_bounds__(kBlockA) void bloom_bin_kernel(BuildArgs a, Keys keys,
+                                                            uint32_t *__restrict__ pos_ws,
+                                                            uint32_t *__restrict__ table_ws) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  const int tid = threadIdx.x;
+  const uint32_t wg = blockIdx.x;
+  const int fi = find_filter_by_chunk(a, wg);
+  const FilterDesc &d = a.f[fi];
+  const uint32_t w = wg - d.chunk_base;
+  const uint32_t C = a.C;
+  const uint32_t k = KFIX > 0 ? (uint32_t)KFIX : a.k;
+  const uint32_t TL = a.TL;
+  const uint32_t first = w * C;
+  const uint32_t cnt = min(C, d.n - first);
+  const uint32_t T = d.tiles;
+  const uint32_t hist_words = (kHistMax + 3) & ~3u;
+  uint32_t *hist = lds;                       // T+1 counters, later cursors
+  uint32_t *scratch = lds + hist_words;       // scan scratch (BLOCK/64 + 1, padded to 32)
+  uint32_t *lpos = lds + hist_words + 32;     // k*C sorted positions
+  const FastMod mod = d.mod;
+
+  for (uint32_t i = tid; i <= T; i += kBlockA) hist[i] = 0;
+
+  uint32_t h1[kKptMax], h2[kKptMax];
+#pragma unroll
+  for (int i = 0; i < kKptMax; ++i) {
+    const uint32_t idx = tid + i * kBlockA;
+    h1[i] = h2[i] = 0;
+    if (idx < cnt) keys.hash(d.key_begin + first + idx, h1[i], h2[i]);
+  }
+  __syncthreads();
+
+  constexpr int KR = KFIX > 0 ? KFIX : 1;
+  uint32_t pos[kKptMax][KR];
+#pragma unroll
+  for (int i = 0; i < kKptMax; ++i) {
+    const uint32_t idx = tid + i * kBlockA;
+    if (idx < cnt) {
+      if constexpr (KFIX > 0) {
+#pragma unroll
+        for (int j = 0; j < KFIX; ++j) {
+          pos[i][j] = fastmod(h1[i] + (uint32_t)j * h2[i], mod);
+          atomicAdd(&hist[pos[i][j] >> TL], 1u);
+        }
+      } else {
+        for (uint32_t j = 0; j < k; ++j) {
+          const uint32_t p = fastmod(h1[i] + j * h2[i], mod);
+          atomicAdd(&hist[p >> TL], 1u);
+        }
+      }
+    }
+  }
+  __syncthreads();
+
+  // Exclusive scan: hist[t] = start of tile t's run; hist[T] = k*cnt.
+  block_excl_scan_array<kBlockA>(hist, T + 1, scratch);
+
+  // (tile, chunk) table, T+1 rows of W entries: row t = start of tile t.
+  uint32_t *tab = table_ws + d.table_base;
+  for (uint32_t t = tid; t <= T; t += kBlockA) tab[(uint64_t)t * d.chunks + w] = hist[t];
+  __syncthreads();
+
+  // Scatter into LDS by tile (hist now serves as the per-tile cursor).
+#pragma unroll
+  for (int i = 0; i < kKptMax; ++i) {
+    const uint32_t idx = tid + i * kBlockA;
+    if (idx < cnt) {
+      if constexpr (KFIX > 0) {
+#pragma unroll
+        for (int j = 0; j < KFIX; ++j) {
+          const uint32_t slot = atomicAdd(&hist[pos[i][j] >> TL], 1u);
+          lpos[slot] = pos[i][j];
+        }
+      } else {
+        for (uint32_t j = 0; j < k; ++j) {
+          const uint32_t p = fastmod(h1[i] + j * h2[i], mod);
+          const uint32_t slot = atomicAdd(&hist[p >> TL], 1u);
+          lpos[slot] = p;
+        }
+      }
+    }
+  }
+  __syncthreads();
+
+  // Stream the sorted chunk out: k*cnt words, region w is k*C words long
+  // (16-byte aligned because C % 4 == 0 and pos_base % 4 == 0).
+  const uint32_t total = k * cnt;
+  uint32_t *dst = pos_ws + d.pos_base + (uint64_t)w * k * C;
+  const uint32_t nvec = total >> 2;
+  const uint4 *src4 = reinterpret_cast<const uint4 *>(lpos);
+  uint4 *dst4 = reinterpret_cast<uint4 *>(dst);
+  for (uint32_t i = tid; i < nvec; i += kBlockA) dst4[i] = src4[i];
+  for (uint32_t i = (nvec << 2) + tid; i < total; i += kBlockA) dst[i] = lpos[i];
+}
+
+// ---------------------------------------------------------------- pass B
+__global__ __launch_bounds__(kBlockB) void bloom_tile_kernel(BuildArgs a,
+                                                             const uint32_t *__restrict__ pos_ws,
+                                                             const uint32_t *__restrict__ table_ws,
+                                                             uint8_t *__restrict__ bitmaps) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  const int tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid / kWave;
+  constexpr int NWAVES = kBlockB / kWave;
+  const uint32_t wg = blockIdx.x;
+  const int fi = find_filter_by_tile(a, wg);
+  const FilterDesc &d = a.f[fi];
+  const uint32_t lt = wg - d.tile_base;
+  const uint32_t TL = a.TL;
+  const uint32_t tile_words = 1u << (TL - 5);
+  const uint32_t tmask = (1u << TL) - 1u;
+  const uint32_t W = d.chunks;
+  const uint32_t k = a.k;
+  const uint32_t region = k * a.C;
+
+  uint32_t *tile = lds;                          // 2^TL bits
+  uint32_t *vstart = lds + tile_words;           // kBlockB + 1 virtual starts
+  uint32_t *segbase = vstart + kBlockB + 4;      // kBlockB segment bases (u32, wrapping)
+  uint32_t *scratch = segbase + kBlockB;         // scan scratch
+
+  for (uint32_t i = tid; i < tile_words; i += kBlockB) tile[i] = 0;
+
+  const uint32_t *row0 = table_ws + d.table_base + (uint64_t)lt * W;
+  const uint32_t *row1 = row0 + W;
+  const uint32_t pos_base = (uint32_t)d.pos_base;
+
+  for (uint32_t wb = 0; wb < W; wb += kBlockB) {
+    const uint32_t nw = min((uint32_t)kBlockB, W - wb);
+    uint32_t s = 0, len = 0;
+    if ((uint32_t)tid < nw) {
+      s = row0[wb + tid];
+      len = row1[wb + tid] - s;
+    }
+    uint32_t L;
+    const uint32_t vs = block_excl_scan<kBlockB>(len, scratch, &L);
+    if ((uint32_t)tid < nw) {
+      vstart[tid] = vs;
+      segbase[tid] = pos_base + (wb + tid) * region + s - vs;  // address = segbase[w] + e
+    }
+    if (tid == 0) vstart[nw] = L;
+    __syncthreads();
+
+    for (uint32_t base = wave * kWave * kUnrollB; base < L; base += NWAVES * kWave * kUnrollB) {
+      const uint32_t e0 = base + lane;
+      uint32_t lo = 0, hi = nw;  // vstart[lo] <= e0 < vstart[hi]
+      while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (vstart[mid] <= e0) lo = mid; else hi = mid;
+      }
+      uint32_t wseg = lo;
+      uint32_t v[kUnrollB];
+#pragma unroll
+      for (int u = 0; u < kUnrollB; ++u) {
+        const uint32_t e = e0 + u * kWave;
+        v[u] = 0xffffffffu;
+        if (e < L) {
+          while (vstart[wseg + 1] <= e) ++wseg;
+          v[u] = pos_ws[segbase[wseg] + e];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < kUnrollB; ++u) {
+        const uint32_t e = e0 + u * kWave;
+        if (e < L) {
+          const uint32_t off = v[u] & tmask;
+          atomicOr(&tile[off >> 5], 1u << (off & 31));
+        }
+      }
+    }
+    __syncthreads();
+  }
+
+  // Write the finished tile: bytes [lt << (TL-3), ...) of this filter, up to the
+  // 16-byte-rounded bitmap length (pad bytes are zero: no position reaches them).
+  const uint64_t tile_bytes = 1ull << (TL - 3);
+  const uint64_t b0 = (uint64_t)lt * tile_bytes;
+  const uint64_t nbytes = min(tile_bytes, (uint64_t)d.alloc_bytes - b0);
+  uint4 *out4 = reinterpret_cast<uint4 *>(bitmaps + d.bitmap_off + b0);
+  const uint4 *t4 = reinterpret_cast<const uint4 *>(tile);
+  for (uint32_t i = tid; i < (uint32_t)(nbytes >> 4); i += kBlockB) out4[i] = t4[i];
+}
+
+// ---------------------------------------------------------------- direct atomics
+template <class Keys>
+__global__ __launch_bounds__(256) void bloom_atomic_kernel(Keys keys, uint64_t n, uint32_t k,
+                                                           FastMod mod, uint32_t *__restrict__ bitmap) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    uint32_t h1, h2;
+    keys.hash(i, h1, h2);
+    for (uint32_t j = 0; j < k; ++j) {
+      const uint32_t p = fastmod(h1 + j * h2, mod);
+      const uint32_t word = p >> 5, bit = 1u << (p & 31);
+      // Test before the atomic: bits only ever go 0 -> 1 within the launch,
+      // so a set bit seen through a stale line is still set.
+      if (!(__builtin_nontemporal_load(bitmap + word) & bit)) atomicOr(bitmap + word, bit);
+    }
+  }
+}
+
+// A view of the key set starting at key `b` (used by the atomic path).
+inline Keys16 shift_keys(Keys16 k, uint64_t b) { k.keys += b; return k; }
+inline KeysStride shift_keys(KeysStride k, uint64_t b) { k.keys += b * k.stride; return k; }
+inline KeysVar shift_keys(KeysVar k, uint64_t b) { k.offs += b; return k; }
+
+// ---------------------------------------------------------------- host plan
+struct Plan {
+  BuildArgs a;
+  uint64_t pos_words = 0, table_words = 0, ws_bytes = 0;
+  uint32_t total_chunks = 0, total_tiles = 0;
+  size_t lds_a = 0, lds_b = 0;
+};
+
+int make_plan(const uint64_t *counts, uint32_t nf, int32_t bpk, Plan &p) {
+  if (nf == 0 || nf > (uint32_t)kMaxFilters || bpk < 0) return ADL_ERR_INVALID_ARG;
+  memset(&p.a, 0, sizeof(p.a));
+  const uint32_t k = (uint32_t)adl_host::num_probes(bpk);
+  uint64_t total_n = 0;
+  for (uint32_t f = 0; f < nf; ++f) {
+    if (adl_host::bitmap_bytes(counts[f], bpk) == 0) return ADL_ERR_TOO_LARGE;
+    total_n += counts[f];
+  }
+  uint32_t cmax = std::min<uint32_t>(kBlockA * kKptMax, kPosLdsWords / k) & ~3u;
+  uint32_t C = cmax;
+  if (total_n / cmax < kTargetWorkgroups) {
+    const uint64_t want = (total_n + kTargetWorkgroups - 1) / kTargetWorkgroups;
+    C = (uint32_t)std::min<uint64_t>(cmax, std::max<uint64_t>(256, adl_host::round_up(want, 4)));
+  }
+  uint32_t TL = kMaxTileLog2;
+  auto tiles_at = [&](uint32_t tl) {
+    uint64_t t = 0;
+    for (uint32_t f = 0; f < nf; ++f) {
+      const uint64_t m = adl_host::bitmap_bytes(counts[f], bpk) * 8;
+      t += (m + (1ull << tl) - 1) >> tl;
+    }
+    return t;
+  };
+  while (TL > kMinTileLog2 && tiles_at(TL) < kTargetWorkgroups) --TL;
+  if (const char *e = getenv("ADL_BLOOM_TILE_LOG2")) {  // tuning override
+    const int v = atoi(e);
+    if (v >= (int)kMinTileLog2 && v <= (int)kMaxTileLog2) TL = (uint32_t)v;
+  }
+  p.a.nf = nf;
+  p.a.k = k;
+  p.a.C = C;
+  p.a.TL = TL;
+  uint64_t pos = 0, tab = 0, boff = 0;
+  uint32_t chunk = 0, tile = 0;
+  for (uint32_t f = 0; f < nf; ++f) {
+    FilterDesc &d = p.a.f[f];
+    const uint64_t bytes = adl_host::bitmap_bytes(counts[f], bpk);
+    const uint32_t m = (uint32_t)(bytes * 8);
+    d.n = (uint32_t)counts[f];
+    d.alloc_bytes = (uint32_t)adl_host::round_up(bytes, 16);
+    d.chunks = (uint32_t)((counts[f] + C - 1) / C);
+    d.tiles = (uint32_t)(((uint64_t)m + (1ull << TL) - 1) >> TL);
+    if (d.tiles + 1 > kHistMax) return ADL_ERR_TOO_LARGE;
+    d.mod = adl_host::make_fastmod(m);
+    d.chunk_base = chunk;
+    d.tile_base = tile;
+    d.pos_base = pos;
+    d.table_base = tab;
+    d.bitmap_off = boff;  // overwritten by the caller
+    d.key_begin = 0;      // overwritten by the caller
+    chunk += d.chunks;
+    tile += d.tiles;
+    pos += (uint64_t)d.chunks * k * C;
+    tab += (uint64_t)(d.tiles + 1) * d.chunks;
+  }
+  if (pos >= (1ull << 32)) return ADL_ERR_TOO_LARGE;  // pass B addresses in u32 words
+  p.total_chunks = chunk;
+  p.total_tiles = tile;
+  p.pos_words = adl_host::round_up(pos, 64);
+  p.table_words = adl_host::round_up(tab, 64);
+  p.ws_bytes = (p.pos_words + p.table_words) * 4 + 256;
+  p.lds_a = (size_t)(((kHistMax + 3) & ~3u) + 32 + k * C) * 4;
+  p.lds_b = (size_t)((1u << (TL - 5)) + (kBlockB + 4) + kBlockB + 32) * 4;
+  return ADL_OK;
+}
+
+// ADL_BLOOM_BUILD_ALGO=atomic selects the direct-atomic build (cross-check and
+// tuning; read per call so tests can switch it).
+bool use_atomic_path() {
+  const char *e = getenv("ADL_BLOOM_BUILD_ALGO");
+  return e && strcmp(e, "atomic") == 0;
+}
+
+// ---------------------------------------------------------------- instrumentation
+// Thread-local event triples (before pass A, between A and B, after B).
+struct Profile {
+  bool on = false;
+  uint32_t used = 0;
+  std::vector<hipEvent_t> ev;  // 3 per build
+  ~Profile() {
+    for (hipEvent_t e : ev) (void)hipEventDestroy(e);
+  }
+};
+thread_local Profile t_prof;
+
+inline hipEvent_t *prof_slot() {
+  if (!t_prof.on || 3 * (t_prof.used + 1) > t_prof.ev.size()) return nullptr;
+  return &t_prof.ev[3 * t_prof.used++];
+}
+
+template <class Keys>
+int launch_binned(const Plan &p, Keys keys, uint8_t *d_bitmaps, void *ws, hipStream_t st) {
+  uint32_t *pos_ws = reinterpret_cast<uint32_t *>(ws);
+  uint32_t *tab_ws = pos_ws + p.pos_words;
+  hipEvent_t *ev = prof_slot();
+  if (ev) ADL_HIP_TRY(hipEventRecord(ev[0], st));
+  if (p.total_chunks) {
+    if (p.a.k == 6) {
+      auto kern = bloom_bin_kernel<6, Keys>;
+      ADL_HIP_TRY(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)p.lds_a));
+      hipLaunchKernelGGL(kern, dim3(p.total_chunks), dim3(kBlockA), p.lds_a, st, p.a, keys, pos_ws, tab_ws);
+    } else {
+      auto kern = bloom_bin_kernel<0, Keys>;
+      ADL_HIP_TRY(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)p.lds_a));
+      hipLaunchKernelGGL(kern, dim3(p.total_chunks), dim3(kBlockA), p.lds_a, st, p.a, keys, pos_ws, tab_ws);
+    }
+    ADL_HIP_TRY(hipGetLastError());
+  }
+  if (ev) ADL_HIP_TRY(hipEventRecord(ev[1], st));
+  ADL_HIP_TRY(hipFuncSetAttribute((const void *)bloom_tile_kernel,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)p.lds_b));
+  hipLaunchKernelGGL(bloom_tile_kernel, dim3(p.total_tiles), dim3(kBlockB), p.lds_b, st, p.a,
+                     (const uint32_t *)pos_ws, (const uint32_t *)tab_ws, d_bitmaps);
+  ADL_HIP_TRY(hipGetLastError());
+  if (ev) ADL_HIP_TRY(hipEventRecord(ev[2], st));
+  return ADL_OK;
+}
+
+template <class Keys>
+int launch_atomic(const Plan &p, Keys keys, uint8_t *d_bitmaps, hipStream_t st) {
+  for (uint32_t f = 0; f < p.a.nf; ++f) {
+    const FilterDesc &d = p.a.f[f];
+    ADL_HIP_TRY(hipMemsetAsync(d_bitmaps + d.bitmap_off, 0, d.alloc_bytes, st));
+    if (d.n == 0) continue;
+    Keys kf = keys;
+    const uint64_t blocks = std::min<uint64_t>((d.n + 255) / 256, 256 * 32);
+    // key_begin offsets are applied through a shifted view
+    hipLaunchKernelGGL(bloom_atomic_kernel<Keys>, dim3((uint32_t)blocks), dim3(256), 0, st,
+                       shift_keys(kf, d.key_begin), (uint64_t)d.n, p.a.k, d.mod,
+                       reinterpret_cast<uint32_t *>(d_bitmaps + d.bitmap_off));
+    ADL_HIP_TRY(hipGetLastError());
+  }
+  return ADL_OK;
+}
+
+}  // namespace
+
+namespace {
+// Runs groups of <= kMaxFilters filters through the plan/launch pair.
+int build_groups(const uint8_t *d_keys, const uint64_t *d_offsets, uint32_t key_stride,
+                 const uint64_t *key_begin, uint32_t num_filters, int32_t bpk, uint8_t *d_bitmaps,
+                 const uint64_t *bitmap_off, void *d_workspace, uint64_t workspace_bytes,
+                 hipStream_t st) {
+  if (!d_keys && key_begin[num_filters] > key_begin[0]) return ADL_ERR_INVALID_ARG;
+  if (!d_offsets && key_stride == 0 && key_begin[num_filters] > key_begin[0]) return ADL_ERR_INVALID_ARG;
+  const bool atomic = use_atomic_path();
+  for (uint32_t g = 0; g < num_filters; g += kMaxFilters) {
+    const uint32_t nf = std::min<uint32_t>(kMaxFilters, num_filters - g);
+    uint64_t counts[kMaxFilters];
+    for (uint32_t f = 0; f < nf; ++f) {
+      if (key_begin[g + f + 1] < key_begin[g + f]) return ADL_ERR_INVALID_ARG;
+      counts[f] = key_begin[g + f + 1] - key_begin[g + f];
+    }
+    Plan p;
+    int rc = make_plan(counts, nf, bpk, p);
+    if (rc) return rc;
+    for (uint32_t f = 0; f < nf; ++f) {
+      if (bitmap_off[g + f] % 16) return ADL_ERR_INVALID_ARG;
+      p.a.f[f].key_begin = key_begin[g + f];
+      p.a.f[f].bitmap_off = bitmap_off[g + f];
+    }
+    if (!atomic && (!d_workspace || workspace_bytes < p.ws_bytes)) return ADL_ERR_WORKSPACE;
+    void *ws = d_workspace;
+    if (ws) ws = reinterpret_cast<void *>(adl_host::round_up(reinterpret_cast<uintptr_t>(ws), 256));
+    if (d_offsets) {
+      KeysVar keys{d_keys, d_offsets};
+      rc = atomic ? launch_atomic(p, keys, d_bitmaps, st) : launch_binned(p, keys, d_bitmaps, ws, st);
+    } else if (key_stride == 16 && (reinterpret_cast<uintptr_t>(d_keys) % 16) == 0) {
+      Keys16 keys{reinterpret_cast<const uint4 *>(d_keys)};
+      rc = atomic ? launch_atomic(p, keys, d_bitmaps, st) : launch_binned(p, keys, d_bitmaps, ws, st);
+    } else {
+      KeysStride keys{d_keys, key_stride};
+      rc = atomic ? launch_atomic(p, keys, d_bitmaps, st) : launch_binned(p, keys, d_bitmaps, ws, st);
+    }
+    if (rc) return rc;
+  }
+  return ADL_OK;
+}
+}  // namespace
+
+// ====================================================================== C-ABI
+extern "C" {
+
+const char *adl_bloom_strerror(int status) {
+  switch (status) {
+    case ADL_OK: return "ok";
+    case ADL_FILTER_BLOCK_ERROR: return "filter block error";
+    case ADL_ERR_INVALID_ARG: return "invalid argument";
+    case ADL_ERR_TOO_LARGE: return "filter too large for the reference's int arithmetic";
+    case ADL_ERR_DEVICE: return "HIP device error";
+    case ADL_ERR_OUT_OF_MEMORY: return "device out of memory";
+    case ADL_ERR_WORKSPACE: return "workspace too small";
+    default: return "unknown error";
+  }
+}
+
+int adl_bloom_abi_version(void) { return ADL_BLOOM_ABI_VERSION; }
+
+int32_t adl_bloom_num_probes(int32_t bits_per_key) { return adl_host::num_probes(bits_per_key); }
+
+uint64_t adl_bloom_bitmap_bytes(uint64_t n, int32_t bits_per_key) {
+  return adl_host::bitmap_bytes(n, bits_per_key);
+}
+
+uint64_t adl_bloom_bitmap_alloc_bytes(uint64_t n, int32_t bits_per_key) {
+  const uint64_t b = adl_host::bitmap_bytes(n, bits_per_key);
+  return b ? adl_host::round_up(b, 16) : 0;
+}
+
+uint64_t adl_bloom_build_workspace_bytes(const uint64_t *key_counts, uint32_t num_filters,
+                                         int32_t bits_per_key) {
+  if (!key_counts) return 0;
+  uint64_t ws = 0;
+  for (uint32_t g = 0; g < num_filters; g += kMaxFilters) {
+    const uint32_t nf = std::min<uint32_t>(kMaxFilters, num_filters - g);
+    Plan p;
+    if (make_plan(key_counts + g, nf, bits_per_key, p)) return 0;
+    ws = std::max(ws, p.ws_bytes);
+  }
+  return ws;
+}
+
+int adl_bloom_build_device(const uint8_t *d_keys, const uint64_t *d_offsets, uint64_t n,
+                           uint32_t key_stride, int32_t bits_per_key, uint8_t *d_bitmap,
+                           void *d_workspace, uint64_t workspace_bytes, void *stream) {
+  try {
+    if (!d_bitmap) return ADL_ERR_INVALID_ARG;
+    if (reinterpret_cast<uintptr_t>(d_bitmap) % 16) return ADL_ERR_INVALID_ARG;
+    const uint64_t kb[2] = {0, n};
+    const uint64_t boff[1] = {0};
+    return build_groups(d_keys, d_offsets, key_stride, kb, 1, bits_per_key, d_bitmap, boff,
+                        d_workspace, workspace_bytes, (hipStream_t)stream);
+  } catch (...) {
+    return ADL_ERR_DEVICE;
+  }
+}
+
+int adl_bloom_build_segmented_device(const uint8_t *d_keys, const uint64_t *d_offsets,
+                                     uint32_t key_stride, const uint64_t *key_begin,
+                                     uint32_t num_filters, int32_t bits_per_key,
+                                     uint8_t *d_bitmaps, const uint64_t *bitmap_off,
+                                     void *d_workspace, uint64_t workspace_bytes, void *stream) {
+  try {
+    if (!key_begin || !bitmap_off || !d_bitmaps || num_filters == 0) return ADL_ERR_INVALID_ARG;
+    if (reinterpret_cast<uintptr_t>(d_bitmaps) % 16) return ADL_ERR_INVALID_ARG;
+    return build_groups(d_keys, d_offsets, key_stride, key_begin, num_filters, bits_per_key,
+                        d_bitmaps, bitmap_off, d_workspace, workspace_bytes, (hipStream_t)stream);
+  } catch (...) {
+    return ADL_ERR_DEVICE;
+  }
+}
+
+int adl_bloom_build(const uint8_t *h_keys, const uint64_t *h_offsets, uint64_t n,
+                    uint32_t key_stride, int32_t bits_per_key, uint8_t *h_bitmap, void *stream) {
+  try {
+    if (!h_bitmap || (n && !h_keys)) return ADL_ERR_INVALID_ARG;
+    if (!h_offsets && n && key_stride == 0) return ADL_ERR_INVALID_ARG;
+    const uint64_t bytes = adl_host::bitmap_bytes(n, bits_per_key);
+    if (!bytes) return bits_per_key < 0 ? ADL_ERR_INVALID_ARG : ADL_ERR_TOO_LARGE;
+    hipStream_t st = (hipStream_t)stream;
+    const uint64_t key_bytes = h_offsets ? (n ? h_offsets[n] : 0) : n * (uint64_t)key_stride;
+    const uint64_t alloc = adl_host::round_up(bytes, 16);
+    const uint64_t ws = adl_bloom_build_workspace_bytes(&n, 1, bits_per_key);
+    // one allocation: [keys | offsets | bitmap | workspace]
+    const uint64_t o_keys = 0;
+    const uint64_t o_offs = adl_host::round_up(key_bytes + 16, 256);
+    const uint64_t o_bm = o_offs + adl_host::round_up(h_offsets ? (n + 1) * 8 : 0, 256);
+    const uint64_t o_ws = o_bm + adl_host::round_up(alloc, 256);
+    const uint64_t total = o_ws + ws;
+    uint8_t *dev = nullptr;
+    ADL_HIP_TRY(hipMallocAsync((void **)&dev, total, st));
+    int rc = ADL_OK;
+    do {
+      if (key_bytes) {
+        if (hipMemcpyAsync(dev + o_keys, h_keys, key_bytes, hipMemcpyHostToDevice, st) != hipSuccess) {
+          rc = ADL_ERR_DEVICE;
+          break;
+        }
+      }
+      if (h_offsets) {
+        if (hipMemcpyAsync(dev + o_offs, h_offsets, (n + 1) * 8, hipMemcpyHostToDevice, st) != hipSuccess) {
+          rc = ADL_ERR_DEVICE;
+          break;
+        }
+      }
+      rc = adl_bloom_build_device(dev + o_keys, h_offsets ? reinterpret_cast<uint64_t *>(dev + o_offs) : nullptr,
+                                  n, key_stride, bits_per_key, dev + o_bm, dev + o_ws, ws, st);
+      if (rc) break;
+      if (hipMemcpyAsync(h_bitmap, dev + o_bm, bytes, hipMemcpyDeviceToHost, st) != hipSuccess) {
+        rc = ADL_ERR_DEVICE;
+        break;
+      }
+    } while (0);
+    (void)hipFreeAsync(dev, st);
+    if (hipStreamSynchronize(st) != hipSuccess && rc == ADL_OK) rc = ADL_ERR_DEVICE;
+    return rc;
+  } catch (...) {
+    return ADL_ERR_DEVICE;
+  }
+}
+
+int adl_bloom_profile_enable(uint32_t capacity) {
+  try {
+    while (t_prof.ev.size() < 3ull * capacity) {
+      hipEvent_t e;
+      ADL_HIP_TRY(hipEventCreate(&e));
+      t_prof.ev.push_back(e);
+    }
+    t_prof.used = 0;
+    t_prof.on = true;
+    return ADL_OK;
+  } catch (...) {
+    return ADL_ERR_DEVICE;
+  }
+}
+
+int adl_bloom_profile_collect(double *ms, uint32_t *builds) {
+  if (!ms || !builds) return ADL_ERR_INVALID_ARG;
+  ms[0] = ms[1] = 0.0;
+  for (uint32_t i = 0; i < t_prof.used; ++i) {
+    hipEvent_t *e = &t_prof.ev[3 * i];
+    float a = 0.f, b = 0.f;
+    ADL_HIP_TRY(hipEventSynchronize(e[2]));
+    ADL_HIP_TRY(hipEventElapsedTime(&a, e[0], e[1]));
+    ADL_HIP_TRY(hipEventElapsedTime(&b, e[1], e[2]));
+    ms[0] += a;
+    ms[1] += b;
+  }
+  *builds = t_prof.used;
+  t_prof.used = 0;
+  t_prof.on = false;
+  return ADL_OK;
+}
+
+}  // extern "C"

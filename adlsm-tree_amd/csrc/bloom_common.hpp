@@ -1,0 +1,142 @@
+// adlsm-tree_amd/csrc/bloom_common.hpp -- shared host/device plumbing of
+// libadlbloom.so: status handling, key-set views, block scans.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/adl_bloom.h"
+#include "murmur3_device.hpp"
+
+#define ADL_HIP_TRY(expr)                                \
+  do {                                                   \
+    hipError_t adl_e_ = (expr);                          \
+    if (adl_e_ != hipSuccess) {                          \
+      return adl_e_ == hipErrorOutOfMemory ? ADL_ERR_OUT_OF_MEMORY : ADL_ERR_DEVICE; \
+    }                                                    \
+  } while (0)
+
+namespace adl_dev {
+
+constexpr int kWave = 64;
+
+// ---------------------------------------------------------------- key views
+// Fixed 16-byte keys, 16-byte aligned: one global_load_dwordx4 per key, so a
+// wave reads 1 KiB contiguous.
+struct Keys16 {
+  const uint4 *keys;
+  __device__ __forceinline__ void hash(uint64_t i, uint32_t &h1, uint32_t &h2) const {
+    hash16(keys[i], h1, h2);
+  }
+};
+
+// Fixed stride (any stride, any alignment).
+struct KeysStride {
+  const uint8_t *keys;
+  uint32_t stride;
+  __device__ __forceinline__ void hash(uint64_t i, uint32_t &h1, uint32_t &h2) const {
+    hash_bytes(keys + i * stride, stride, kSeed1, kSeed2, h1, h2);
+  }
+};
+
+// Variable length: key i = keys[offs[i] .. offs[i+1]).
+struct KeysVar {
+  const uint8_t *keys;
+  const uint64_t *offs;
+  __device__ __forceinline__ void hash(uint64_t i, uint32_t &h1, uint32_t &h2) const {
+    const uint64_t o0 = offs[i], o1 = offs[i + 1];
+    hash_bytes(keys + o0, (uint32_t)(o1 - o0), kSeed1, kSeed2, h1, h2);
+  }
+};
+
+// ---------------------------------------------------------------- scans
+// Inclusive wave64 scan.
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {
+#pragma unroll
+  for (int off = 1; off < kWave; off <<= 1) {
+    uint32_t t = __shfl_up(v, off, kWave);
+    if (lane >= off) v += t;
+  }
+  return v;
+}
+
+// Exclusive scan of one value per thread over the block.  `scratch` holds
+// BLOCK/64 + 1 words of LDS.  Returns the exclusive prefix; *total = sum.
+template <int BLOCK>
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *scratch, uint32_t *total) {
+  const int tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid / kWave;
+  constexpr int NW = BLOCK / kWave;
+  const uint32_t incl = wave_incl_scan(v, lane);
+  if (lane == kWave - 1) scratch[wave] = incl;
+  __syncthreads();
+  if (wave == 0) {
+    uint32_t w = lane < NW ? scratch[lane] : 0u;
+    uint32_t wi = wave_incl_scan(w, lane);
+    if (lane < NW) scratch[lane] = wi - w;
+    if (lane == NW - 1) scratch[NW] = wi;
+  }
+  __syncthreads();
+  const uint32_t r = scratch[wave] + incl - v;
+  *total = scratch[NW];
+  __syncthreads();  // scratch may be reused right after
+  return r;
+}
+
+// In-place exclusive scan of an LDS array a[0..N), N <= BLOCK * 4 entries per
+// thread; returns the total.  Each thread owns a contiguous run.
+template <int BLOCK>
+__device__ __forceinline__ uint32_t block_excl_scan_array(uint32_t *a, uint32_t N, uint32_t *scratch) {
+  const uint32_t per = (N + BLOCK - 1) / BLOCK;
+  const uint32_t beg = threadIdx.x * per;
+  const uint32_t end = beg + per < N ? beg + per : N;
+  uint32_t s = 0;
+  for (uint32_t i = beg; i < end; ++i) s += a[i];
+  uint32_t total;
+  uint32_t run = block_excl_scan<BLOCK>(s, scratch, &total);
+  for (uint32_t i = beg; i < end; ++i) {
+    const uint32_t v = a[i];
+    a[i] = run;
+    run += v;
+  }
+  __syncthreads();
+  return total;
+}
+
+}  // namespace adl_dev
+
+namespace adl_host {
+
+// Host-side magic numbers for adl_dev::fastmod (see murmur3_device.hpp).
+inline adl_dev::FastMod make_fastmod(uint32_t m) {
+  adl_dev::FastMod f{};
+  f.m = m;
+  if ((m & (m - 1u)) == 0u) {
+    f.pow2 = 1;
+    f.magic = 0;
+    f.shift = 0;
+    return f;
+  }
+  uint32_t l = 0;
+  while ((1ull << l) < m) ++l;  // ceil(log2 m)
+  f.pow2 = 0;
+  f.magic = (uint32_t)((((1ull << 32) * ((1ull << l) - m)) / m) + 1ull);
+  f.shift = l - 1;
+  return f;
+}
+
+inline int num_probes(int32_t bpk) {
+  int k = (int)(bpk * 0.69);  // src/filter_block.cpp:44
+  if (k < 1) k = 1;
+  if (k > 30) k = 30;
+  return k;
+}
+
+inline uint64_t bitmap_bytes(uint64_t n, int32_t bpk) {
+  if (bpk < 0) return 0;
+  const uint64_t bytes = n * (uint64_t)bpk + 7;
+  if (n > 0x7fffffffull || bytes * 8 > 0x7fffffffull) return 0;
+  return bytes;
+}
+
+inline uint64_t round_up(uint64_t v, uint64_t a) { return (v + a - 1) / a * a; }
+
+}  // namespace adl_host

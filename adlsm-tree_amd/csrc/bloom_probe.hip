@@ -1,0 +1,406 @@
+// adlsm-tree_amd/csrc/bloom_probe.hip -- MI355X (gfx950) batched bloom probe,
+// batched murmur3 and the device-side synthetic key generators.
+//
+// Probe replaces BloomFilter::IsKeyExists (reference src/filter_block.cpp:49-62)
+// for a batch: m = bitmap_bytes*8 (:50), the same h1 + j*h2 positions as the
+// build, "absent" at the first clear bit (:54-59).  One query per lane; the key
+// load is coalesced, the k bitmap reads are random byte loads that stop at the
+// first clear bit (the same early exit as the reference).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+#include <cmath>
+#include <new>
+
+#include "bloom_common.hpp"
+
+using namespace adl_dev;
+
+namespace {
+
+constexpr int kBlockP = 256;
+
+template <class Keys>
+__global__ __launch_bounds__(kBlockP) void bloom_probe_kernel(Keys keys, uint64_t n, uint32_t k,
+                                                              FastMod mod,
+                                                              const uint8_t *__restrict__ bitmap,
+                                                              uint8_t *__restrict__ out) {
+  for (uint64_t i = blockIdx.x * (uint64_t)kBlockP + threadIdx.x; i < n;
+       i += (uint64_t)gridDim.x * kBlockP) {
+    uint32_t h1, h2;
+    keys.hash(i, h1, h2);
+    uint8_t hit = 1;
+    for (uint32_t j = 0; j < k; ++j) {
+      const uint32_t p = fastmod(h1 + j * h2, mod);
+      if (!((bitmap[p >> 3] >> (p & 7)) & 1u)) {
+        hit = 0;
+        break;
+      }
+    }
+    out[i] = hit;
+  }
+}
+
+// Multi-filter probe: per-query divisor, so the remainder is the hardware-free
+// 32-bit `%` sequence instead of a launch-constant magic multiply.
+template <class Keys>
+__global__ __launch_bounds__(kBlockP) void bloom_probe_multi_kernel(
+    Keys keys, uint64_t n, uint32_t k, const uint32_t *__restrict__ fid, uint32_t nf,
+    const uint8_t *__restrict__ bitmaps, const uint64_t *__restrict__ boff,
+    uint8_t *__restrict__ out) {
+  for (uint64_t i = blockIdx.x * (uint64_t)kBlockP + threadIdx.x; i < n;
+       i += (uint64_t)gridDim.x * kBlockP) {
+    const uint32_t f = fid[i];
+    uint8_t hit = 0;
+    if (f < nf) {
+      const uint64_t b0 = boff[f], b1 = boff[f + 1];
+      const uint32_t m = (uint32_t)((b1 - b0) * 8);
+      const uint8_t *bm = bitmaps + b0;
+      uint32_t h1, h2;
+      keys.hash(i, h1, h2);
+      hit = m != 0;
+      for (uint32_t j = 0; j < k && hit; ++j) {
+        const uint32_t p = (h1 + j * h2) % m;
+        if (!((bm[p >> 3] >> (p & 7)) & 1u)) hit = 0;
+      }
+    }
+    out[i] = hit;
+  }
+}
+
+template <class Keys>
+__global__ __launch_bounds__(kBlockP) void murmur3_batch_kernel(Keys keys, uint64_t n,
+                                                                uint32_t *__restrict__ out) {
+  for (uint64_t i = blockIdx.x * (uint64_t)kBlockP + threadIdx.x; i < n;
+       i += (uint64_t)gridDim.x * kBlockP) {
+    uint32_t a, b;
+    keys.hash(i, a, b);
+    out[2 * i] = a;
+    out[2 * i + 1] = b;
+  }
+}
+
+// Arbitrary seeds (the key views hash with the filter's two seeds).
+__global__ __launch_bounds__(kBlockP) void murmur3_seeded_kernel(const uint8_t *__restrict__ keys,
+                                                                 const uint64_t *__restrict__ offs,
+                                                                 uint32_t stride, uint64_t n,
+                                                                 uint32_t sa, uint32_t sb,
+                                                                 uint32_t *__restrict__ out) {
+  for (uint64_t i = blockIdx.x * (uint64_t)kBlockP + threadIdx.x; i < n;
+       i += (uint64_t)gridDim.x * kBlockP) {
+    const uint64_t o0 = offs ? offs[i] : i * stride;
+    const uint32_t len = offs ? (uint32_t)(offs[i + 1] - o0) : stride;
+    uint32_t a, b;
+    hash_bytes(keys + o0, len, sa, sb, a, b);
+    out[2 * i] = a;
+    out[2 * i + 1] = b;
+  }
+}
+
+// ---------------------------------------------------------------- synthetic data
+__device__ __forceinline__ uint64_t splitmix_at(uint64_t seed, uint64_t call /* 1-based */) {
+  uint64_t z = seed + call * 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+__global__ __launch_bounds__(256) void synth_keys16_kernel(uint4 *__restrict__ out, uint64_t seed,
+                                                           uint64_t skip, uint64_t n) {
+  for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+    const uint64_t c = 2 * (skip + i);
+    const uint64_t a = splitmix_at(seed, c + 1), b = splitmix_at(seed, c + 2);
+    out[i] = make_uint4((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32));
+  }
+}
+
+constexpr int kZipfR = 249;  // lengths 8 .. 256
+
+__global__ __launch_bounds__(256) void synth_lengths_kernel(uint32_t *__restrict__ len, uint64_t seed,
+                                                            uint64_t n, double s) {
+  __shared__ double cdf[kZipfR];
+  if (threadIdx.x == 0) {
+    double acc = 0;
+    for (int r = 1; r <= kZipfR; ++r) {
+      acc += pow((double)r, -s);
+      cdf[r - 1] = acc;
+    }
+    for (int r = 0; r < kZipfR; ++r) cdf[r] /= acc;
+  }
+  __syncthreads();
+  const uint64_t lseed = seed ^ 0xD1B54A32D192ED03ull;
+  for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+    const double u = (double)(splitmix_at(lseed, i + 1) >> 11) * (1.0 / 9007199254740992.0);
+    int lo = 0, hi = kZipfR - 1;  // first r with u < cdf[r]
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (u < cdf[mid]) hi = mid; else lo = mid + 1;
+    }
+    len[i] = 8u + (uint32_t)lo;
+  }
+}
+
+__global__ __launch_bounds__(256) void synth_fill_kernel(uint64_t *__restrict__ out, uint64_t seed,
+                                                         uint64_t words) {
+  for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < words; i += (uint64_t)gridDim.x * 256)
+    out[i] = splitmix_at(seed, i + 1);
+}
+
+inline uint32_t grid_for(uint64_t n, int block) {
+  return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n + block - 1) / block, 256ull * 64));
+}
+
+template <class F>
+int dispatch_keys(const uint8_t *d_keys, const uint64_t *d_offsets, uint32_t key_stride, F &&fn) {
+  if (d_offsets) return fn(KeysVar{d_keys, d_offsets});
+  if (key_stride == 16 && reinterpret_cast<uintptr_t>(d_keys) % 16 == 0)
+    return fn(Keys16{reinterpret_cast<const uint4 *>(d_keys)});
+  return fn(KeysStride{d_keys, key_stride});
+}
+
+}  // namespace
+
+extern "C" {
+
+int adl_bloom_probe_device(const uint8_t *d_keys, const uint64_t *d_offsets, uint64_t n,
+                           uint32_t key_stride, int32_t bits_per_key, const uint8_t *d_bitmap,
+                           uint64_t bitmap_bytes, uint8_t *d_out, void *stream) {
+  if (n == 0) return ADL_OK;
+  if (!d_keys || !d_bitmap || !d_out || bits_per_key < 0) return ADL_ERR_INVALID_ARG;
+  if (!d_offsets && key_stride == 0) return ADL_ERR_INVALID_ARG;
+  if (bitmap_bytes == 0) return ADL_ERR_INVALID_ARG;  // h % 0 is undefined in the reference
+  if (bitmap_bytes * 8 > 0x7fffffffull) return ADL_ERR_TOO_LARGE;
+  const uint32_t k = (uint32_t)adl_host::num_probes(bits_per_key);
+  const FastMod mod = adl_host::make_fastmod((uint32_t)(bitmap_bytes * 8));
+  hipStream_t st = (hipStream_t)stream;
+  return dispatch_keys(d_keys, d_offsets, key_stride, [&](auto keys) -> int {
+    hipLaunchKernelGGL(bloom_probe_kernel<decltype(keys)>, dim3(grid_for(n, kBlockP)), dim3(kBlockP), 0,
+                       st, keys, n, k, mod, d_bitmap, d_out);
+    ADL_HIP_TRY(hipGetLastError());
+    return ADL_OK;
+  });
+}
+
+int adl_bloom_probe_multi_device(const uint8_t *d_keys, const uint64_t *d_offsets, uint64_t n,
+                                 uint32_t key_stride, const uint32_t *d_filter_id,
+                                 uint32_t num_filters, const uint8_t *d_bitmaps,
+                                 const uint64_t *d_bitmap_off, int32_t bits_per_key,
+                                 uint8_t *d_out, void *stream) {
+  if (n == 0) return ADL_OK;
+  if (!d_keys || !d_filter_id || !d_out || bits_per_key < 0) return ADL_ERR_INVALID_ARG;
+  if (num_filters && (!d_bitmaps || !d_bitmap_off)) return ADL_ERR_INVALID_ARG;
+  if (!d_offsets && key_stride == 0) return ADL_ERR_INVALID_ARG;
+  const uint32_t k = (uint32_t)adl_host::num_probes(bits_per_key);
+  hipStream_t st = (hipStream_t)stream;
+  return dispatch_keys(d_keys, d_offsets, key_stride, [&](auto keys) -> int {
+    hipLaunchKernelGGL(bloom_probe_multi_kernel<decltype(keys)>, dim3(grid_for(n, kBlockP)),
+                       dim3(kBlockP), 0, st, keys, n, k, d_filter_id, num_filters, d_bitmaps,
+                       d_bitmap_off, d_out);
+    ADL_HIP_TRY(hipGetLastError());
+    return ADL_OK;
+  });
+}
+
+int adl_bloom_probe(const uint8_t *h_keys, const uint64_t *h_offsets, uint64_t n,
+                    uint32_t key_stride, int32_t bits_per_key, const uint8_t *h_bitmap,
+                    uint64_t bitmap_bytes, uint8_t *h_out, void *stream) {
+  if (n == 0) return ADL_OK;
+  if (!h_keys || !h_bitmap || !h_out) return ADL_ERR_INVALID_ARG;
+  if (!h_offsets && key_stride == 0) return ADL_ERR_INVALID_ARG;
+  hipStream_t st = (hipStream_t)stream;
+  const uint64_t key_bytes = h_offsets ? h_offsets[n] : n * (uint64_t)key_stride;
+  const uint64_t o_offs = adl_host::round_up(key_bytes + 16, 256);
+  const uint64_t o_bm = o_offs + adl_host::round_up(h_offsets ? (n + 1) * 8 : 0, 256);
+  const uint64_t o_out = o_bm + adl_host::round_up(bitmap_bytes, 256);
+  const uint64_t total = o_out + adl_host::round_up(n, 256);
+  uint8_t *dev = nullptr;
+  ADL_HIP_TRY(hipMallocAsync((void **)&dev, total, st));
+  int rc = ADL_OK;
+  do {
+    if (hipMemcpyAsync(dev, h_keys, key_bytes, hipMemcpyHostToDevice, st) != hipSuccess ||
+        (h_offsets && hipMemcpyAsync(dev + o_offs, h_offsets, (n + 1) * 8, hipMemcpyHostToDevice,
+                                     st) != hipSuccess) ||
+        hipMemcpyAsync(dev + o_bm, h_bitmap, bitmap_bytes, hipMemcpyHostToDevice, st) != hipSuccess) {
+      rc = ADL_ERR_DEVICE;
+      break;
+    }
+    rc = adl_bloom_probe_device(dev, h_offsets ? reinterpret_cast<uint64_t *>(dev + o_offs) : nullptr,
+                                n, key_stride, bits_per_key, dev + o_bm, bitmap_bytes, dev + o_out, st);
+    if (rc) break;
+    if (hipMemcpyAsync(h_out, dev + o_out, n, hipMemcpyDeviceToHost, st) != hipSuccess) rc = ADL_ERR_DEVICE;
+  } while (0);
+  (void)hipFreeAsync(dev, st);
+  if (hipStreamSynchronize(st) != hipSuccess && rc == ADL_OK) rc = ADL_ERR_DEVICE;
+  return rc;
+}
+
+int adl_bloom_murmur3_device(const uint8_t *d_keys, const uint64_t *d_offsets, uint64_t n,
+                             uint32_t key_stride, uint32_t seed_a, uint32_t seed_b,
+                             uint32_t *d_out, void *stream) {
+  if (n == 0) return ADL_OK;
+  if (!d_keys || !d_out || (!d_offsets && key_stride == 0)) return ADL_ERR_INVALID_ARG;
+  hipStream_t st = (hipStream_t)stream;
+  if (seed_a == kSeed1 && seed_b == kSeed2) {
+    return dispatch_keys(d_keys, d_offsets, key_stride, [&](auto keys) -> int {
+      hipLaunchKernelGGL(murmur3_batch_kernel<decltype(keys)>, dim3(grid_for(n, kBlockP)),
+                         dim3(kBlockP), 0, st, keys, n, d_out);
+      ADL_HIP_TRY(hipGetLastError());
+      return ADL_OK;
+    });
+  }
+  hipLaunchKernelGGL(murmur3_seeded_kernel, dim3(grid_for(n, kBlockP)), dim3(kBlockP), 0, st, d_keys,
+                     d_offsets, key_stride, n, seed_a, seed_b, d_out);
+  ADL_HIP_TRY(hipGetLastError());
+  return ADL_OK;
+}
+
+int adl_bloom_murmur3(uint32_t seed, const void *data, uint64_t len, uint32_t *h_out) {
+  if (!h_out || (len && !data) || len > 0xffffffffull) return ADL_ERR_INVALID_ARG;
+  uint8_t *dev = nullptr;
+  const uint64_t o_out = adl_host::round_up(len + 16, 256);
+  ADL_HIP_TRY(hipMalloc((void **)&dev, o_out + 16));
+  int rc = ADL_OK;
+  uint32_t res[2] = {0, 0};
+  if ((len && hipMemcpy(dev, data, len, hipMemcpyHostToDevice) != hipSuccess)) rc = ADL_ERR_DEVICE;
+  if (rc == ADL_OK) {
+    hipLaunchKernelGGL(murmur3_seeded_kernel, dim3(1), dim3(kBlockP), 0, (hipStream_t)0, dev,
+                       (const uint64_t *)nullptr, (uint32_t)len, 1ull, seed, seed,
+                       reinterpret_cast<uint32_t *>(dev + o_out));
+    if (hipGetLastError() != hipSuccess ||
+        hipMemcpy(res, dev + o_out, 8, hipMemcpyDeviceToHost) != hipSuccess)
+      rc = ADL_ERR_DEVICE;
+  }
+  (void)hipFree(dev);
+  if (rc == ADL_OK) *h_out = res[0];
+  return rc;
+}
+
+int adl_synth_keys16_device(uint8_t *d_out, uint64_t seed, uint64_t skip, uint64_t n, void *stream) {
+  if (n == 0) return ADL_OK;
+  if (!d_out || reinterpret_cast<uintptr_t>(d_out) % 16) return ADL_ERR_INVALID_ARG;
+  hipLaunchKernelGGL(synth_keys16_kernel, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream,
+                     reinterpret_cast<uint4 *>(d_out), seed, skip, n);
+  ADL_HIP_TRY(hipGetLastError());
+  return ADL_OK;
+}
+
+int adl_synth_varlen_lengths_device(uint32_t *d_lengths, uint64_t seed, uint64_t n, double zipf_s,
+                                    void *stream) {
+  if (n == 0) return ADL_OK;
+  if (!d_lengths) return ADL_ERR_INVALID_ARG;
+  hipLaunchKernelGGL(synth_lengths_kernel, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream,
+                     d_lengths, seed, n, zipf_s);
+  ADL_HIP_TRY(hipGetLastError());
+  return ADL_OK;
+}
+
+int adl_synth_varlen_fill_device(uint8_t *d_out, uint64_t seed, uint64_t total_bytes, void *stream) {
+  if (total_bytes == 0) return ADL_OK;
+  if (!d_out || reinterpret_cast<uintptr_t>(d_out) % 8) return ADL_ERR_INVALID_ARG;
+  const uint64_t words = (total_bytes + 7) / 8;  // caller allocates round_up(total_bytes, 8)
+  hipLaunchKernelGGL(synth_fill_kernel, dim3(grid_for(words, 256)), dim3(256), 0, (hipStream_t)stream,
+                     reinterpret_cast<uint64_t *>(d_out), seed, words);
+  ADL_HIP_TRY(hipGetLastError());
+  return ADL_OK;
+}
+
+}  // extern "C"
+
+// ====================================================================== filter sets
+struct adl_bloom_filter_set {
+  uint8_t *d_bitmaps = nullptr;
+  uint64_t *d_off = nullptr;
+  uint32_t nf = 0;
+  int32_t bpk = 0;
+};
+
+extern "C" {
+
+int adl_bloom_filter_set_create(const uint8_t *h_bitmaps, const uint64_t *h_bitmap_off,
+                                uint32_t num_filters, int32_t bits_per_key,
+                                adl_bloom_filter_set **out) {
+  if (!out || !h_bitmap_off || bits_per_key < 0) return ADL_ERR_INVALID_ARG;
+  *out = nullptr;
+  const uint64_t total = h_bitmap_off[num_filters];
+  for (uint32_t f = 0; f < num_filters; ++f)
+    if (h_bitmap_off[f + 1] < h_bitmap_off[f]) return ADL_ERR_INVALID_ARG;
+  if (total && !h_bitmaps) return ADL_ERR_INVALID_ARG;
+  auto *s = new (std::nothrow) adl_bloom_filter_set;
+  if (!s) return ADL_ERR_OUT_OF_MEMORY;
+  s->nf = num_filters;
+  s->bpk = bits_per_key;
+  int rc = ADL_OK;
+  if (hipMalloc((void **)&s->d_bitmaps, total + 16) != hipSuccess ||
+      hipMalloc((void **)&s->d_off, (num_filters + 1) * sizeof(uint64_t)) != hipSuccess) {
+    rc = ADL_ERR_OUT_OF_MEMORY;
+  } else if ((total && hipMemcpy(s->d_bitmaps, h_bitmaps, total, hipMemcpyHostToDevice) != hipSuccess) ||
+             hipMemcpy(s->d_off, h_bitmap_off, (num_filters + 1) * sizeof(uint64_t),
+                       hipMemcpyHostToDevice) != hipSuccess) {
+    rc = ADL_ERR_DEVICE;
+  }
+  if (rc) {
+    adl_bloom_filter_set_destroy(s);
+    return rc;
+  }
+  *out = s;
+  return ADL_OK;
+}
+
+int adl_bloom_filter_set_probe(const adl_bloom_filter_set *set, const uint8_t *h_keys,
+                               const uint64_t *h_offsets, uint64_t n, uint32_t key_stride,
+                               const uint32_t *h_filter_id, uint32_t filter, uint8_t *h_out,
+                               void *stream) {
+  if (!set) return ADL_ERR_INVALID_ARG;
+  if (n == 0) return ADL_OK;
+  if (!h_keys || !h_out || (!h_offsets && key_stride == 0)) return ADL_ERR_INVALID_ARG;
+  hipStream_t st = (hipStream_t)stream;
+  const uint64_t key_bytes = h_offsets ? h_offsets[n] : n * (uint64_t)key_stride;
+  const uint64_t o_offs = adl_host::round_up(key_bytes + 16, 256);
+  const uint64_t o_fid = o_offs + adl_host::round_up(h_offsets ? (n + 1) * 8 : 0, 256);
+  const uint64_t o_out = o_fid + adl_host::round_up(n * 4, 256);
+  const uint64_t total = o_out + adl_host::round_up(n, 256);
+  uint8_t *dev = nullptr;
+  ADL_HIP_TRY(hipMallocAsync((void **)&dev, total, st));
+  int rc = ADL_OK;
+  do {
+    uint32_t *d_fid = reinterpret_cast<uint32_t *>(dev + o_fid);
+    if ((key_bytes && hipMemcpyAsync(dev, h_keys, key_bytes, hipMemcpyHostToDevice, st) != hipSuccess) ||
+        (h_offsets && hipMemcpyAsync(dev + o_offs, h_offsets, (n + 1) * 8, hipMemcpyHostToDevice,
+                                     st) != hipSuccess) ||
+        (h_filter_id && hipMemcpyAsync(d_fid, h_filter_id, n * 4, hipMemcpyHostToDevice, st) != hipSuccess) ||
+        (!h_filter_id && hipMemsetD32Async((hipDeviceptr_t)d_fid, (int)filter, n, st) != hipSuccess)) {
+      rc = ADL_ERR_DEVICE;
+      break;
+    }
+    rc = adl_bloom_probe_multi_device(dev, h_offsets ? reinterpret_cast<uint64_t *>(dev + o_offs) : nullptr,
+                                      n, key_stride, d_fid, set->nf, set->d_bitmaps, set->d_off,
+                                      set->bpk, dev + o_out, st);
+    if (rc) break;
+    if (hipMemcpyAsync(h_out, dev + o_out, n, hipMemcpyDeviceToHost, st) != hipSuccess) rc = ADL_ERR_DEVICE;
+  } while (0);
+  (void)hipFreeAsync(dev, st);
+  if (hipStreamSynchronize(st) != hipSuccess && rc == ADL_OK) rc = ADL_ERR_DEVICE;
+  return rc;
+}
+
+int adl_bloom_filter_set_device_view(const adl_bloom_filter_set *set, const uint8_t **d_bitmaps,
+                                     const uint64_t **d_bitmap_off, uint32_t *num_filters) {
+  if (!set) return ADL_ERR_INVALID_ARG;
+  if (d_bitmaps) *d_bitmaps = set->d_bitmaps;
+  if (d_bitmap_off) *d_bitmap_off = set->d_off;
+  if (num_filters) *num_filters = set->nf;
+  return ADL_OK;
+}
+
+int adl_bloom_filter_set_destroy(adl_bloom_filter_set *set) {
+  if (!set) return ADL_OK;
+  int rc = ADL_OK;
+  if (set->d_bitmaps && hipFree(set->d_bitmaps) != hipSuccess) rc = ADL_ERR_DEVICE;
+  if (set->d_off && hipFree(set->d_off) != hipSuccess) rc = ADL_ERR_DEVICE;
+  delete set;
+  return rc;
+}
+
+}  // extern "C"

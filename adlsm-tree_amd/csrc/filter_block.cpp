@@ -1,0 +1,259 @@
+// adlsm-tree_amd/csrc/filter_block.cpp -- host C++ mirror of the reference's
+// filter API over the gfx950 C-ABI (include/adl_bloom.h).  See
+// filter_block.hpp for what differs from src/filter_block.cpp underneath.
+#include "filter_block.hpp"
+
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "adl_bloom.h"
+
+namespace adl {
+
+namespace {
+
+/* Decode32 (reference src/encode.cpp:6): native-endian unaligned int32 load. */
+int Load32(const char *src) {
+  int v;
+  memcpy(&v, src, sizeof(int));
+  return v;
+}
+
+void Append32(string &dst, int v) { dst.append(reinterpret_cast<const char *>(&v), sizeof(int)); }
+
+RC FromStatus(int status) {
+  if (status == ADL_OK) return OK;
+  if (status == ADL_FILTER_BLOCK_ERROR) return FILTER_BLOCK_ERROR;
+  if (status == ADL_ERR_TOO_LARGE) return OUT_OF_RANGE;
+  return DEVICE_ERROR;
+}
+
+void Pack(const vector<string> &keys, KeyArena &arena) {
+  for (const auto &k : keys) arena.Add(k);
+}
+
+}  // namespace
+
+string_view strrc(RC rc) {
+  static const char *const kNames[] = {
+      "ok", "not found", "is not directory", "create directory failed",
+      "destroy directory failed", "destroy file failed", "un implemented", "existed",
+      "open file error", "io error", "close file error", "rename file error",
+      "make temp error", "filter block error", "footer block error", "unsupported format",
+      "db closed", "stat file error", "mmap error", "out of range", "bad level",
+      "bad revision", "bad file meta", "bad record", "file eof", "check sum error",
+      "noexcept size", "bad file path", "bad current file", "new sstable error",
+      "device error"};
+  if (rc >= 0 && rc <= DEVICE_ERROR) return kNames[rc];
+  return "unknown error";
+}
+
+// ------------------------------------------------------------- BloomFilter
+
+/* src/filter_block.cpp:35-47 -- k from bits_per_key (same formula, in the C-ABI). */
+BloomFilter::BloomFilter(int bits_per_key)
+    : bits_per_key_(bits_per_key), k_(adl_bloom_num_probes(bits_per_key)) {}
+
+/* src/filter_block.cpp:9-33 -- appends n*bpk+7 bytes of bitmap to `result`. */
+RC BloomFilter::Keys2Block(const vector<string> &keys, string &result) {
+  KeyArena arena;
+  Pack(keys, arena);
+  return Keys2Block(arena, result);
+}
+
+RC BloomFilter::Keys2Block(const KeyArena &keys, string &result) {
+  const uint64_t n = keys.size();
+  const uint64_t bytes = adl_bloom_bitmap_bytes(n, bits_per_key_);
+  if (bytes == 0) return OUT_OF_RANGE;
+  const size_t init_len = result.size();
+  result.resize(init_len + bytes);
+  const int st = adl_bloom_build(reinterpret_cast<const uint8_t *>(keys.bytes().data()),
+                                 keys.offsets().data(), n, 0, bits_per_key_,
+                                 reinterpret_cast<uint8_t *>(&result[init_len]), nullptr);
+  if (st != ADL_OK) {
+    result.resize(init_len);
+    return FromStatus(st);
+  }
+  return OK;
+}
+
+/* src/filter_block.cpp:49-62 -- one key against a host bitmap view.  The
+ * bitmap is not resident, so this uploads it; FilterBlockReader keeps its
+ * bitmaps on the device instead.  A device failure answers true ("may be
+ * present"), the answer that never loses a key. */
+bool BloomFilter::IsKeyExists(string_view key, string_view bitmap) {
+  if (bitmap.empty()) return false;
+  const uint64_t offs[2] = {0, key.size()};
+  const char empty = 0;
+  uint8_t hit = 1;
+  const int st = adl_bloom_probe(reinterpret_cast<const uint8_t *>(key.empty() ? &empty : key.data()),
+                                 offs, 1, 0, bits_per_key_,
+                                 reinterpret_cast<const uint8_t *>(bitmap.data()), bitmap.size(),
+                                 &hit, nullptr);
+  if (st != ADL_OK) {
+    fprintf(stderr, "adl::BloomFilter::IsKeyExists: %s\n", adl_bloom_strerror(st));
+    return true;
+  }
+  return hit != 0;
+}
+
+RC BloomFilter::IsKeysExist(const KeyArena &keys, string_view bitmap, vector<uint8_t> &out) {
+  out.assign(keys.size(), 0);
+  if (keys.empty()) return OK;
+  if (bitmap.empty()) return OK;
+  const int st = adl_bloom_probe(reinterpret_cast<const uint8_t *>(keys.bytes().data()),
+                                 keys.offsets().data(), keys.size(), 0, bits_per_key_,
+                                 reinterpret_cast<const uint8_t *>(bitmap.data()), bitmap.size(),
+                                 out.data(), nullptr);
+  return FromStatus(st);
+}
+
+/* src/filter_block.cpp:64-67 -- "bf:" + raw native-endian int32 bits_per_key. */
+void BloomFilter::FilterInfo(string &info) {
+  info.append("bf:");
+  Append32(info, bits_per_key_);
+}
+
+// ------------------------------------------------------------- FilterBlockWriter
+
+FilterBlockWriter::FilterBlockWriter(unique_ptr<FilterAlgorithm> &&method)
+    : method_(std::move(method)) {}
+
+/* src/filter_block.cpp:72-75 */
+RC FilterBlockWriter::Update(string_view key) {
+  keys_.Add(key);
+  return OK;
+}
+
+/* src/filter_block.cpp:104-109 -- one GPU build for the whole pending batch. */
+RC FilterBlockWriter::Keys2Block() {
+  offsets_.push_back((int)buffer_.size());
+  RC rc = method_->Keys2Block(keys_, buffer_);
+  keys_.Clear();
+  if (rc != OK && status_ == OK) status_ = rc;
+  return rc;
+}
+
+/* src/filter_block.cpp:77-102 -- [bitmaps][int32 offsets][int32 offsets_start]
+ * [int32 num_filters][info]["int32 info_len"], moved out into `result`.
+ * Returns the first Keys2Block failure (the reference cannot fail here). */
+RC FilterBlockWriter::Final(string &result) {
+  if (!keys_.empty()) Keys2Block();
+  const int offsets_start = (int)buffer_.size();
+  for (int off : offsets_) Append32(buffer_, off);
+  Append32(buffer_, offsets_start);
+  Append32(buffer_, (int)offsets_.size());
+  string info;
+  method_->FilterInfo(info);
+  if (!info.empty()) {
+    buffer_.append(info);
+    Append32(buffer_, (int)info.size());
+  }
+  result = std::move(buffer_);
+  buffer_.clear();
+  offsets_.clear();
+  RC rc = status_;
+  status_ = OK;
+  return rc;
+}
+
+// ------------------------------------------------------------- FilterBlockReader
+
+FilterBlockReader::FilterBlockReader() : filters_nums_(0), filters_offsets_offset_(0) {}
+
+FilterBlockReader::~FilterBlockReader() { adl_bloom_filter_set_destroy(device_set_); }
+
+/* src/filter_block.cpp:113-155 -- same trailer walk and the same
+ * FILTER_BLOCK_ERROR checks, plus bounds checks where the reference would read
+ * outside the block; then the bitmaps are uploaded once (Upload). */
+RC FilterBlockReader::Init(string_view filter_blocks) {
+  filter_blocks_ = filter_blocks;
+  const int64_t len = (int64_t)filter_blocks_.size();
+  if (len < (int64_t)sizeof(int)) return FILTER_BLOCK_ERROR;
+  const int info_len_offset = (int)(len - sizeof(int));
+  const int info_len = Load32(&filter_blocks_[info_len_offset]);
+  if (info_len > info_len_offset || info_len <= 0) return FILTER_BLOCK_ERROR;
+  const int info_offset = info_len_offset - info_len;
+  filter_info_ = filter_blocks_.substr(info_offset, info_len);
+  if (RC rc = CreateFilterAlgorithm(); rc) return rc;
+  if (info_offset < (int)sizeof(int)) return FILTER_BLOCK_ERROR;
+  const int nums_offset = info_offset - (int)sizeof(int);
+  filters_nums_ = Load32(&filter_blocks_[nums_offset]);
+  if (nums_offset < (int)sizeof(int)) return FILTER_BLOCK_ERROR;
+  filters_offsets_offset_ = Load32(&filter_blocks_[nums_offset - sizeof(int)]);
+  if (filters_offsets_offset_ < 0) return FILTER_BLOCK_ERROR;
+  if (filters_nums_ < 0 ||
+      (int64_t)filters_offsets_offset_ + (int64_t)sizeof(int) * (filters_nums_ ? filters_nums_ : 1) >
+          nums_offset)
+    return FILTER_BLOCK_ERROR; /* the reference reads out of bounds here */
+  if (Load32(&filter_blocks_[filters_offsets_offset_]) != 0) return FILTER_BLOCK_ERROR;
+  filters_offsets_ = filter_blocks_.substr(filters_offsets_offset_, sizeof(int) * filters_nums_);
+  return Upload();
+}
+
+/* src/filter_block.cpp:158-170 -- only "bf" is known; bits_per_key at info[3]. */
+RC FilterBlockReader::CreateFilterAlgorithm() {
+  if (filter_info_.substr(0, 2) != "bf") return FILTER_BLOCK_ERROR;
+  if (filter_info_.size() < 3 + sizeof(int)) return FILTER_BLOCK_ERROR;
+  bits_per_key_ = Load32(&filter_info_[3]);
+  method_ = std::make_unique<BloomFilter>(bits_per_key_);
+  return OK;
+}
+
+RC FilterBlockReader::Upload() {
+  adl_bloom_filter_set_destroy(device_set_);
+  device_set_ = nullptr;
+  vector<uint64_t> off(filters_nums_ + 1);
+  for (int i = 0; i < filters_nums_; ++i) {
+    const int o = Load32(&filters_offsets_[i * sizeof(int)]);
+    if (o < 0 || o > filters_offsets_offset_ || (i && (uint64_t)o < off[i - 1])) return FILTER_BLOCK_ERROR;
+    off[i] = (uint64_t)o;
+  }
+  off[filters_nums_] = (uint64_t)filters_offsets_offset_;
+  const int st = adl_bloom_filter_set_create(reinterpret_cast<const uint8_t *>(filter_blocks_.data()),
+                                             off.data(), (uint32_t)filters_nums_, bits_per_key_,
+                                             &device_set_);
+  return FromStatus(st);
+}
+
+/* src/filter_block.cpp:172-184 -- one key against filter `filter_block_num`.
+ * A device failure answers true ("may be present"). */
+bool FilterBlockReader::IsKeyExists(int filter_block_num, string_view key) {
+  if (filter_block_num < 0 || filter_block_num >= filters_nums_ || !device_set_) return false;
+  const uint64_t offs[2] = {0, key.size()};
+  const char empty = 0;
+  uint8_t hit = 1;
+  const int st = adl_bloom_filter_set_probe(
+      device_set_, reinterpret_cast<const uint8_t *>(key.empty() ? &empty : key.data()), offs, 1, 0,
+      nullptr, (uint32_t)filter_block_num, &hit, nullptr);
+  if (st != ADL_OK) {
+    fprintf(stderr, "adl::FilterBlockReader::IsKeyExists: %s\n", adl_bloom_strerror(st));
+    return true;
+  }
+  return hit != 0;
+}
+
+RC FilterBlockReader::IsKeysExist(int filter_block_num, const KeyArena &keys, vector<uint8_t> &out) {
+  out.assign(keys.size(), 0);
+  if (filter_block_num < 0 || filter_block_num >= filters_nums_ || keys.empty()) return OK;
+  if (!device_set_) return FILTER_BLOCK_ERROR;
+  const int st = adl_bloom_filter_set_probe(
+      device_set_, reinterpret_cast<const uint8_t *>(keys.bytes().data()), keys.offsets().data(),
+      keys.size(), 0, nullptr, (uint32_t)filter_block_num, out.data(), nullptr);
+  return FromStatus(st);
+}
+
+/* src/murmur3_hash.cpp:11-65, evaluated on the GPU.  There is no error channel
+ * in this signature, so a device failure aborts loudly. */
+uint32_t murmur3_hash(uint32_t seed, const char *data, size_t len) {
+  uint32_t h = 0;
+  const int st = adl_bloom_murmur3(seed, data, len, &h);
+  if (st != ADL_OK) {
+    fprintf(stderr, "adl::murmur3_hash: %s\n", adl_bloom_strerror(st));
+    abort();
+  }
+  return h;
+}
+
+}  // namespace adl

@@ -1,0 +1,92 @@
+// adlsm-tree_amd/csrc/filter_block_test.cpp -- the scenario of the reference's
+// test/filter_block_test.cpp:4-53, run against the gfx950-backed C++ mirror
+// (filter_block.hpp).  Needs a GPU.  Exit status 0 = every check passed.
+// With argv[1], the finished filter block is also written to that file so
+// tests/test_gpu_parity.py can compare it byte for byte with the oracle.
+#include <stdio.h>
+
+#include <fstream>
+#include <string>
+
+#include "filter_block.hpp"
+
+static int g_failures = 0;
+#define CHECK(cond)                                                       \
+  do {                                                                    \
+    if (!(cond)) {                                                        \
+      fprintf(stderr, "%s:%d: check failed: %s\n", __FILE__, __LINE__, #cond); \
+      ++g_failures;                                                       \
+    }                                                                     \
+  } while (0)
+
+int main(int argc, char **argv) {
+  using namespace adl;
+  FilterBlockWriter writer(make_unique<BloomFilter>(10));
+
+  // filter 0: four named keys and "hello-ddl0" .. "hello-ddl9999"
+  for (const char *k : {"hello", "world", "hello-yly", "hello-ddl"}) CHECK(writer.Update(k) == OK);
+  for (int i = 0; i < 10000; ++i) writer.Update("hello-ddl" + std::to_string(i));
+  CHECK(writer.Keys2Block() == OK);
+
+  // filter 1: three keys
+  for (const char *k : {"adl", "dont", "like-apple"}) writer.Update(k);
+  CHECK(writer.Keys2Block() == OK);
+
+  std::string block;
+  CHECK(writer.Final(block) == OK);
+  CHECK(block.size() == 100111u);
+
+  FilterBlockReader reader;
+  CHECK(reader.Init(block) == OK);
+  CHECK(reader.filters_nums() == 2);
+
+  // the reference's assertions (test/filter_block_test.cpp:37-52)
+  CHECK(!reader.IsKeyExists(0, "adl"));
+  CHECK(!reader.IsKeyExists(0, "zackboge"));
+  CHECK(reader.IsKeyExists(0, "hello-yly"));
+  CHECK(reader.IsKeyExists(0, "hello-ddl"));
+  CHECK(reader.IsKeyExists(0, "hello"));
+  CHECK(reader.IsKeyExists(0, "world"));
+  KeyArena batch;
+  for (int i = 0; i < 10000; ++i) batch.Add("hello-ddl" + std::to_string(i));
+  std::vector<uint8_t> hits;
+  CHECK(reader.IsKeysExist(0, batch, hits) == OK);
+  int positives = 0;
+  for (uint8_t h : hits) positives += h;
+  CHECK(positives == 10000);
+  CHECK(reader.IsKeyExists(1, "adl"));
+  CHECK(reader.IsKeyExists(1, "dont"));
+  CHECK(reader.IsKeyExists(1, "like-apple"));
+  CHECK(!reader.IsKeyExists(1, "dont like-apple"));
+  CHECK(!reader.IsKeyExists(2, "adl"));  // filter index out of range -> false (:174)
+
+  // the non-resident path (BloomFilter::IsKeyExists on a host bitmap view)
+  BloomFilter bf(10);
+  std::string bm;
+  CHECK(bf.Keys2Block(std::vector<std::string>{"adl", "dont", "like-apple"}, bm) == OK);
+  CHECK(bm.size() == 37u);
+  CHECK(bf.IsKeyExists("adl", bm));
+  CHECK(!bf.IsKeyExists("dont like-apple", bm));
+
+  // murmur3_hash on the GPU
+  CHECK(murmur3_hash(0xe2c6928au, "hello", 5) == 0x6d84082cu);
+  CHECK(murmur3_hash(0xbaea8a8fu, "hello", 5) == 0xc6ba3a6bu);
+  CHECK(murmur3_hash(0xe2c6928au, "", 0) == 0x389d2042u);
+
+  // malformed blocks are rejected, as in src/filter_block.cpp:118-144
+  FilterBlockReader bad;
+  CHECK(bad.Init(std::string("abc")) == FILTER_BLOCK_ERROR);
+  std::string wrong_type = block;
+  wrong_type[wrong_type.size() - 11] = 'x';  // "bf:" -> "xf:"
+  CHECK(bad.Init(wrong_type) == FILTER_BLOCK_ERROR);
+
+  if (argc > 1) {
+    std::ofstream(argv[1], std::ios::binary).write(block.data(), (std::streamsize)block.size());
+  }
+  if (g_failures) {
+    fprintf(stderr, "filter_block_test: %d check(s) failed\n", g_failures);
+    return 1;
+  }
+  printf("filter_block_test: all checks passed\n");
+  return 0;
+}

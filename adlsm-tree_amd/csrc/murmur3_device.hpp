@@ -1,0 +1,132 @@
+// adlsm-tree_amd/csrc/murmur3_device.hpp -- gfx950 device form of the
+// reference's MurmurHash3 variant (src/murmur3_hash.cpp:5-65).
+//
+// The reference is NOT canonical MurmurHash3:
+//   * each data byte is a signed char, sign-extended to 32 bits before it is
+//     shifted and ORed into the block word (src/murmur3_hash.cpp:26-29), and
+//     XORed into the tail word (:43-49);
+//   * rotate_left works on a signed int, so its right shift is arithmetic
+//     (src/murmur3_hash.cpp:5-9).
+// Both quirks are reproduced bit-exactly here.  Block words are produced from
+// four raw little-endian bytes in one 32-bit register with a branch-free fill
+// instead of four sign-extending byte loads.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace adl_dev {
+
+constexpr uint32_t kSeed1 = 0xe2c6928au;  // src/filter_block.cpp:22
+constexpr uint32_t kSeed2 = 0xbaea8a8fu;  // src/filter_block.cpp:23
+
+// (uint32_t)d[0] | (uint32_t)d[1] << 8 | ... with signed d[i]: the lowest byte
+// whose sign bit is set sign-extends over every byte above it.
+__device__ __forceinline__ uint32_t quirk_word(uint32_t raw) {
+  uint32_t s = raw & 0x80808080u;
+  uint32_t lowest = s & (0u - s);            // sign bit of the lowest negative byte
+  uint32_t fill = ~((lowest << 1) - 1u);     // all bits above that byte (0 if none)
+  return raw | fill;
+}
+
+// rotate_left(int value, 15|13) with arithmetic >> (src/murmur3_hash.cpp:5-9).
+template <int C>
+__device__ __forceinline__ uint32_t rotl_quirk(uint32_t x) {
+  return (x << C) | (uint32_t)((int32_t)x >> (32 - C));
+}
+
+__device__ __forceinline__ uint32_t mix_block(uint32_t h, uint32_t k) {
+  k *= 0xcc9e2d51u;       // :31
+  k = rotl_quirk<15>(k);  // :32
+  k *= 0x1b873593u;       // :33
+  h ^= k;                 // :35
+  return rotl_quirk<13>(h) * 5u + 0xe6546b64u;  // :36
+}
+
+__device__ __forceinline__ uint32_t mix_tail(uint32_t h, uint32_t k1) {
+  k1 *= 0xcc9e2d51u;  // :50-53
+  k1 = rotl_quirk<15>(k1);
+  k1 *= 0x1b873593u;
+  return h ^ k1;
+}
+
+__device__ __forceinline__ uint32_t fmix(uint32_t h, uint32_t len) {
+  h ^= len;  // :57-62
+  h ^= h >> 16;
+  h *= 0x85ebca6bu;
+  h ^= h >> 13;
+  h *= 0xc2b2ae35u;
+  h ^= h >> 16;
+  return h;
+}
+
+__device__ __forceinline__ uint32_t sx8(uint32_t byte) { return (uint32_t)(int32_t)(int8_t)byte; }
+
+// Tail word for len & 3 in {1,2,3}: k1 ^= sx(t2)<<16; k1 ^= sx(t1)<<8; k1 ^= sx(t0)
+// (src/murmur3_hash.cpp:41-49).  `raw` holds the tail bytes little-endian.
+__device__ __forceinline__ uint32_t tail_word(uint32_t raw, uint32_t rem) {
+  uint32_t k1 = 0;
+  if (rem >= 3) k1 ^= sx8((raw >> 16) & 0xff) << 16;
+  if (rem >= 2) k1 ^= sx8((raw >> 8) & 0xff) << 8;
+  k1 ^= sx8(raw & 0xff);
+  return k1;
+}
+
+// Both seeds of a 16-byte key held as four raw little-endian words.
+__device__ __forceinline__ void hash16(uint4 raw, uint32_t &h1, uint32_t &h2) {
+  const uint32_t w0 = quirk_word(raw.x), w1 = quirk_word(raw.y);
+  const uint32_t w2 = quirk_word(raw.z), w3 = quirk_word(raw.w);
+  uint32_t a = kSeed1, b = kSeed2;
+  a = mix_block(a, w0); b = mix_block(b, w0);
+  a = mix_block(a, w1); b = mix_block(b, w1);
+  a = mix_block(a, w2); b = mix_block(b, w2);
+  a = mix_block(a, w3); b = mix_block(b, w3);
+  h1 = fmix(a, 16u);
+  h2 = fmix(b, 16u);
+}
+
+// Unaligned little-endian 32-bit read of 4 bytes (global or LDS generic pointer).
+__device__ __forceinline__ uint32_t load_u32_unaligned(const uint8_t *p) {
+  uint32_t v;
+  __builtin_memcpy(&v, p, 4);
+  return v;
+}
+
+// Both seeds of an arbitrary-length key at byte pointer p (any alignment).
+__device__ __forceinline__ void hash_bytes(const uint8_t *p, uint32_t len, uint32_t seed_a,
+                                           uint32_t seed_b, uint32_t &ha, uint32_t &hb) {
+  uint32_t a = seed_a, b = seed_b;
+  const uint32_t nblk = len >> 2;
+  for (uint32_t i = 0; i < nblk; ++i) {
+    const uint32_t w = quirk_word(load_u32_unaligned(p + 4 * i));
+    a = mix_block(a, w);
+    b = mix_block(b, w);
+  }
+  const uint32_t rem = len & 3u;
+  if (rem) {
+    const uint8_t *t = p + 4 * nblk;
+    uint32_t raw = t[0];
+    if (rem >= 2) raw |= (uint32_t)t[1] << 8;
+    if (rem >= 3) raw |= (uint32_t)t[2] << 16;
+    const uint32_t k1 = tail_word(raw, rem);
+    a = mix_tail(a, k1);
+    b = mix_tail(b, k1);
+  }
+  ha = fmix(a, len);
+  hb = fmix(b, len);
+}
+
+// h % m for a launch-constant divisor 1 <= m < 2^31 (Granlund-Montgomery
+// round-up method, exact for every 32-bit numerator): q = (t + ((h-t)>>1)) >> (l-1),
+// t = mulhi(h, magic).  For m a power of two (l == 0 path) magic = 0, shift = log2 m.
+struct FastMod {
+  uint32_t m, magic, shift, pow2;
+};
+
+__device__ __forceinline__ uint32_t fastmod(uint32_t h, const FastMod &d) {
+  if (d.pow2) return h & (d.m - 1u);
+  const uint32_t t = __umulhi(h, d.magic);
+  const uint32_t q = (t + ((h - t) >> 1)) >> d.shift;
+  return h - q * d.m;
+}
+
+}  // namespace adl_dev

@@ -1,0 +1,203 @@
+/*
+ * include/adl_bloom.h -- C-ABI of the MI355X (gfx950) SSTable bloom-filter
+ * build/probe layer (libadlbloom.so).
+ *
+ * This is the drop-in boundary for the reference's filter path
+ * (adlternative/adlsm-tree):
+ *   - src/murmur3_hash.hpp:9        uint32_t murmur3_hash(seed, data, len)
+ *   - src/filter_block.hpp:22-34    class BloomFilter : FilterAlgorithm
+ *       Keys2Block(const vector<string>&, string&)   (src/filter_block.cpp:9-33)
+ *       IsKeyExists(string_view key, string_view bm) (src/filter_block.cpp:49-62)
+ *   - src/filter_block.hpp:36-73    FilterBlockWriter / FilterBlockReader
+ * The host C++ mirror of those classes (adlsm-tree_amd/csrc/filter_block.hpp)
+ * and any FFI binding (ctypes) call only what is declared
+ * here: plain pointers and sizes, no C++ or torch types, no exceptions.
+ *
+ * Key sets are packed: `keys` is a byte buffer; key i is
+ *   keys[offsets[i] .. offsets[i+1])          when offsets != NULL (n+1 entries)
+ *   keys[i*key_stride .. (i+1)*key_stride)    when offsets == NULL
+ * Bitmaps are the reference's bytes exactly: n*bits_per_key + 7 bytes, bit b
+ * of the filter is bit (b & 7) of byte (b >> 3).
+ *
+ * Every function returns an adl_status (0 = OK).  All entry points are
+ * re-entrant and thread-safe: work is enqueued on the caller's HIP stream
+ * (`stream`, a hipStream_t; NULL = the null stream) and nothing global is
+ * mutated after the once-guarded device query.  Functions named *_device take
+ * device pointers and do not synchronise; the others take host pointers and
+ * return when the results are in host memory.
+ */
+#ifndef ADL_BLOOM_H_
+#define ADL_BLOOM_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ADL_BLOOM_ABI_VERSION 1
+
+/* Status codes.  ADL_OK and ADL_FILTER_BLOCK_ERROR keep the values of the
+ * reference's enum RC (src/rc.hpp:8-39: OK = 0, FILTER_BLOCK_ERROR = 13); the
+ * negative codes are device/argument failures the CPU reference cannot have. */
+typedef enum adl_status {
+  ADL_OK = 0,
+  ADL_FILTER_BLOCK_ERROR = 13, /* malformed filter block (src/filter_block.cpp:113-170) */
+  ADL_ERR_INVALID_ARG = -1,    /* NULL pointer, negative bits_per_key, bad offsets/alignment */
+  ADL_ERR_TOO_LARGE = -2,      /* n*bits_per_key+7 exceeds the reference's int range */
+  ADL_ERR_DEVICE = -3,         /* HIP runtime / launch failure, no GPU */
+  ADL_ERR_OUT_OF_MEMORY = -4,  /* device allocation failed */
+  ADL_ERR_WORKSPACE = -5       /* caller workspace smaller than required */
+} adl_status;
+
+/* Human-readable text for a status (static storage). */
+const char *adl_bloom_strerror(int status);
+
+/* ABI version of the loaded library (== ADL_BLOOM_ABI_VERSION). */
+int adl_bloom_abi_version(void);
+
+/* k = (int)(bits_per_key * 0.69) clamped to [1, 30]  (src/filter_block.cpp:44-46). */
+int32_t adl_bloom_num_probes(int32_t bits_per_key);
+
+/* Bitmap size in bytes, n*bits_per_key + 7 (src/filter_block.cpp:11-14); 0 when
+ * the reference's `int` arithmetic would overflow or bits_per_key < 0. */
+uint64_t adl_bloom_bitmap_bytes(uint64_t n, int32_t bits_per_key);
+
+/* Device buffer size a *_device build writes for one filter: the bitmap rounded
+ * up to 16 bytes (the pad bytes are written as zero). */
+uint64_t adl_bloom_bitmap_alloc_bytes(uint64_t n, int32_t bits_per_key);
+
+/* ---------------------------------------------------------------- build */
+
+/* Workspace (device bytes) adl_bloom_build_device / _segmented_device need for
+ * filters with the given key counts (num_filters entries).  key_counts is a
+ * HOST array. */
+uint64_t adl_bloom_build_workspace_bytes(const uint64_t *key_counts, uint32_t num_filters,
+                                         int32_t bits_per_key);
+
+/* Build one filter from device-resident keys into a device bitmap.
+ * Replaces BloomFilter::Keys2Block (src/filter_block.cpp:9-33) for a batch.
+ *   d_bitmap: adl_bloom_bitmap_alloc_bytes(n, bpk) bytes, 16-byte aligned;
+ *             every byte is written (no pre-zeroing needed).
+ *   d_workspace: adl_bloom_build_workspace_bytes(&n, 1, bpk) bytes, 256-B aligned. */
+int adl_bloom_build_device(const uint8_t *d_keys, const uint64_t *d_offsets, uint64_t n,
+                           uint32_t key_stride, int32_t bits_per_key, uint8_t *d_bitmap,
+                           void *d_workspace, uint64_t workspace_bytes, void *stream);
+
+/* Build num_filters independent filters (one per SSTable) in one pass pair.
+ * Filter f owns keys [key_begin[f], key_begin[f+1]) of the key set and writes
+ * its bitmap at d_bitmaps + bitmap_off[f] (16-byte aligned, room for
+ * adl_bloom_bitmap_alloc_bytes(n_f, bpk)).  key_begin (num_filters+1 entries)
+ * and bitmap_off (num_filters entries) are HOST arrays. */
+int adl_bloom_build_segmented_device(const uint8_t *d_keys, const uint64_t *d_offsets,
+                                     uint32_t key_stride, const uint64_t *key_begin,
+                                     uint32_t num_filters, int32_t bits_per_key,
+                                     uint8_t *d_bitmaps, const uint64_t *bitmap_off,
+                                     void *d_workspace, uint64_t workspace_bytes, void *stream);
+
+/* Host-pointer convenience: upload keys, build, download exactly
+ * adl_bloom_bitmap_bytes(n, bpk) bytes into h_bitmap (which may be unaligned,
+ * e.g. the tail of a std::string as in Keys2Block).  Synchronous. */
+int adl_bloom_build(const uint8_t *h_keys, const uint64_t *h_offsets, uint64_t n,
+                    uint32_t key_stride, int32_t bits_per_key, uint8_t *h_bitmap,
+                    void *stream);
+
+/* ---------------------------------------------------------------- probe */
+
+/* Probe n keys against one device bitmap of bitmap_bytes bytes (the exact
+ * reference length; m = bitmap_bytes*8 as in src/filter_block.cpp:50).
+ * d_out[i] = 1 if key i may be present, 0 if it is certainly absent.
+ * Replaces BloomFilter::IsKeyExists (src/filter_block.cpp:49-62) for a batch. */
+int adl_bloom_probe_device(const uint8_t *d_keys, const uint64_t *d_offsets, uint64_t n,
+                           uint32_t key_stride, int32_t bits_per_key, const uint8_t *d_bitmap,
+                           uint64_t bitmap_bytes, uint8_t *d_out, void *stream);
+
+/* Probe n keys, key i against filter d_filter_id[i] of num_filters resident
+ * bitmaps; filter f is d_bitmaps[d_bitmap_off[f] .. d_bitmap_off[f+1]) (device
+ * array, num_filters+1 entries).  A filter id >= num_filters answers 0, as
+ * FilterBlockReader::IsKeyExists does (src/filter_block.cpp:174). */
+int adl_bloom_probe_multi_device(const uint8_t *d_keys, const uint64_t *d_offsets, uint64_t n,
+                                 uint32_t key_stride, const uint32_t *d_filter_id,
+                                 uint32_t num_filters, const uint8_t *d_bitmaps,
+                                 const uint64_t *d_bitmap_off, int32_t bits_per_key,
+                                 uint8_t *d_out, void *stream);
+
+/* Host-pointer convenience for adl_bloom_probe_device.  Synchronous. */
+int adl_bloom_probe(const uint8_t *h_keys, const uint64_t *h_offsets, uint64_t n,
+                    uint32_t key_stride, int32_t bits_per_key, const uint8_t *h_bitmap,
+                    uint64_t bitmap_bytes, uint8_t *h_out, void *stream);
+
+/* ------------------------------------------------- device-resident filter sets */
+
+/* A set of filters resident in device memory (the reader side: one set per
+ * SSTable filter block, or many SSTables' filters for a multi-get).  Replaces
+ * the mmapped, non-owning bitmaps FilterBlockReader probes
+ * (src/filter_block.cpp:172-184, src/sstable.cpp:195-204). */
+typedef struct adl_bloom_filter_set adl_bloom_filter_set;
+
+/* Upload num_filters bitmaps: filter f = h_bitmaps[h_bitmap_off[f] ..
+ * h_bitmap_off[f+1]) (HOST arrays, num_filters+1 offsets).  Synchronous. */
+int adl_bloom_filter_set_create(const uint8_t *h_bitmaps, const uint64_t *h_bitmap_off,
+                                uint32_t num_filters, int32_t bits_per_key,
+                                adl_bloom_filter_set **out);
+
+/* Probe n host keys; key i against filter h_filter_id[i], or against
+ * `filter` for every key when h_filter_id is NULL.  h_out[i] = 0/1.
+ * Synchronous on `stream`. */
+int adl_bloom_filter_set_probe(const adl_bloom_filter_set *set, const uint8_t *h_keys,
+                               const uint64_t *h_offsets, uint64_t n, uint32_t key_stride,
+                               const uint32_t *h_filter_id, uint32_t filter, uint8_t *h_out,
+                               void *stream);
+
+/* Device views of a set, for callers that keep queries on the device and call
+ * adl_bloom_probe_multi_device themselves. */
+int adl_bloom_filter_set_device_view(const adl_bloom_filter_set *set, const uint8_t **d_bitmaps,
+                                     const uint64_t **d_bitmap_off, uint32_t *num_filters);
+
+int adl_bloom_filter_set_destroy(adl_bloom_filter_set *set);
+
+/* ---------------------------------------------------------------- hash */
+
+/* The reference's murmur3 variant (src/murmur3_hash.cpp:11-65) on the GPU for a
+ * batch: d_out[2i] = murmur3_hash(seed_a, key_i), d_out[2i+1] = (seed_b, key_i). */
+int adl_bloom_murmur3_device(const uint8_t *d_keys, const uint64_t *d_offsets, uint64_t n,
+                             uint32_t key_stride, uint32_t seed_a, uint32_t seed_b,
+                             uint32_t *d_out, void *stream);
+
+/* Single-key form of murmur3_hash(seed, data, len) (src/murmur3_hash.hpp:9),
+ * computed on the GPU.  Synchronous; on failure *h_out is left untouched. */
+int adl_bloom_murmur3(uint32_t seed, const void *data, uint64_t len, uint32_t *h_out);
+
+/* ---------------------------------------------------------------- instrumentation */
+
+/* Per-kernel timing of the build for the calling thread: while enabled, each
+ * build records HIP events on its stream around pass A (bloom_bin_kernel) and
+ * pass B (bloom_tile_kernel); up to `capacity` builds are kept.  collect()
+ * synchronises on the recorded events, writes the summed milliseconds of the
+ * two kernels to ms[0] (pass A) and ms[1] (pass B), the number of timed builds
+ * to *builds, and disables timing.  Used by bench.py for the live roofline. */
+int adl_bloom_profile_enable(uint32_t capacity);
+int adl_bloom_profile_collect(double *ms, uint32_t *builds);
+
+/* ---------------------------------------------------------------- synthetic data */
+
+/* SURVEY.md §8d SplitMix64 16-byte keys, generated on the device: key i of the
+ * stream seeded `seed`, skipping the first `skip` keys, = LE64(next) || LE64(next). */
+int adl_synth_keys16_device(uint8_t *d_out, uint64_t seed, uint64_t skip, uint64_t n,
+                            void *stream);
+
+/* Variable-length synthetic keys (DESIGN.md "Synthetic inputs"): lengths
+ * 8 + (r-1), r ~ Zipf(s) on [1, 249] by inverse CDF over a SplitMix64 counter
+ * stream; d_lengths (n entries, uint32) must then be prefix-summed by the
+ * caller into offsets, after which adl_synth_varlen_fill_device writes the
+ * bytes (byte j of the packed buffer = byte j%8 of SplitMix64 output j/8). */
+int adl_synth_varlen_lengths_device(uint32_t *d_lengths, uint64_t seed, uint64_t n, double zipf_s,
+                                    void *stream);
+int adl_synth_varlen_fill_device(uint8_t *d_out, uint64_t seed, uint64_t total_bytes, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* ADL_BLOOM_H_ */

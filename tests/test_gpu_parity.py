@@ -1,0 +1,328 @@
+"""GPU parity: the gfx950 kernels (through the C-ABI) against the oracle and the
+reference's golden vectors.  Bit-exact everywhere (integer / byte work).
+
+Sizes: the oracle finishes each case in well under a second, except the
+10M-key headline build, which is checked against the reference's own SHA-256
+(tests/golden/appendix_b.json) instead of re-running the oracle.
+"""
+import hashlib
+import os
+import random
+import subprocess
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def dev():
+    import torch
+
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    torch.cuda.set_device(0)
+    return torch
+
+
+@pytest.fixture(scope="module")
+def ab():
+    import adlbloom
+
+    adlbloom.lib()
+    return adlbloom
+
+
+def to_dev(torch, a):
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def packed_dev(torch, keys):
+    import oracle as O
+
+    data, offs = O.pack(keys)
+    pad = np.zeros(((data.size + 15) // 16) * 16 + 16, dtype=np.uint8)
+    pad[: data.size] = data
+    return to_dev(torch, pad), to_dev(torch, offs.view(np.int64)), data, offs
+
+
+def rand_keys(rng, n, lo, hi, alphabet=None):
+    out = []
+    for _ in range(n):
+        L = rng.randrange(lo, hi + 1)
+        if alphabet is None:
+            out.append(bytes(rng.randrange(256) for _ in range(L)))
+        else:
+            out.append(bytes(rng.choice(alphabet) for _ in range(L)))
+    return out
+
+
+# ----------------------------------------------------------------- murmur3
+def test_murmur3_device_vs_reference_vectors(dev, ab, golden):
+    vecs = golden["murmur3"]["vectors"]
+    keys = [bytes.fromhex(v["key"]) for v in vecs]
+    dk, do, _, _ = packed_dev(dev, keys)
+    got = ab.murmur3_batch(dk, do).cpu().numpy().view(np.uint32)
+    assert [int(x) for x in got[:, 0]] == [v["h1"] for v in vecs]
+    assert [int(x) for x in got[:, 1]] == [v["h2"] for v in vecs]
+    got0 = ab.murmur3_batch(dk, do, seed_a=0, seed_b=0).cpu().numpy().view(np.uint32)
+    assert [int(x) for x in got0[:, 0]] == [v["s0"] for v in vecs]
+
+
+def test_murmur3_single_key_kat(dev, ab, golden):
+    for v in golden["appendix_b"]["murmur3_kat"]:
+        k = bytes.fromhex(v["key"])
+        assert ab.murmur3(ab.SEED1, k) == int(v["h1"], 16)
+        assert ab.murmur3(ab.SEED2, k) == int(v["h2"], 16)
+
+
+def test_murmur3_fixed16_vs_oracle(dev, ab, oracle):
+    keys = ab.synth_keys16(50000, seed=123)
+    got = ab.murmur3_batch(keys).cpu().numpy().view(np.uint32)
+    assert np.array_equal(got, oracle.murmur3_batch(keys.cpu().numpy()))
+
+
+def test_synth_keys_match_survey_generator(dev, ab, oracle):
+    for seed, skip in [(0x5EED, 0), (0x5EED, 777), (0xFEED, 3)]:
+        k = ab.synth_keys16(4096, seed=seed, skip=skip).cpu().numpy()
+        assert np.array_equal(k, oracle.splitmix_keys16(seed, 4096, skip=skip))
+
+
+# ----------------------------------------------------------------- build, 16 B keys
+@pytest.mark.parametrize("idx", range(5))
+def test_build_matches_appendix_b(dev, ab, golden, oracle, idx):
+    g = golden["appendix_b"]["bitmaps"][idx]
+    keys = ab.synth_keys16(g["n"], seed=0x5EED)
+    bm = ab.build(keys, bits_per_key=10).cpu().numpy()
+    assert bm.size == g["bytes"]
+    assert hashlib.sha256(bm.tobytes()).hexdigest() == g["sha256"]
+    assert np.array_equal(bm, oracle.keys2block(keys.cpu().numpy()))
+
+
+def test_build_10m_headline_matches_reference_sha(dev, ab, golden):
+    g = golden["appendix_b"]["bitmaps"][5]
+    assert g["n"] == 10_000_000
+    keys = ab.synth_keys16(g["n"], seed=0x5EED)
+    b = ab.Builder(g["n"], 10)
+    for _ in range(3):  # repeated builds into the same buffers stay exact
+        bm = b.build(keys).cpu().numpy()
+        assert bm.size == g["bytes"]
+        assert int(np.unpackbits(bm).sum()) == g["popcount"]
+        assert hashlib.sha256(bm.tobytes()).hexdigest() == g["sha256"]
+    # size-independent property: every inserted key probes positive
+    assert bool(ab.probe(keys, b.bitmap, nbytes=g["bytes"]).all().item())
+
+
+@pytest.mark.parametrize("n", [0, 1, 2, 3, 63, 64, 65, 1023, 6143, 6144, 6145, 12289, 250_001])
+def test_build_sizes_vs_oracle(dev, ab, oracle, n):
+    keys = ab.synth_keys16(n, seed=0xABC + n)
+    bm = ab.build(keys, bits_per_key=10).cpu().numpy()
+    assert np.array_equal(bm, oracle.keys2block(keys.cpu().numpy().reshape(n, 16)))
+
+
+@pytest.mark.parametrize("bpk", [0, 1, 2, 3, 5, 8, 9, 10, 11, 12, 16, 20, 30, 44, 50])
+def test_build_bits_per_key_sweep(dev, ab, oracle, bpk):
+    n = 20011
+    keys = ab.synth_keys16(n, seed=bpk + 1)
+    bm = ab.build(keys, bits_per_key=bpk).cpu().numpy()
+    assert np.array_equal(bm, oracle.keys2block(keys.cpu().numpy(), bits_per_key=bpk))
+
+
+@pytest.mark.parametrize("tl", [10, 11, 13, 15, 17, 19, 20])
+def test_build_tile_size_invariance(dev, ab, oracle, tl, monkeypatch):
+    monkeypatch.setenv("ADL_BLOOM_TILE_LOG2", str(tl))
+    keys = ab.synth_keys16(150_000, seed=99)
+    bm = ab.build(keys).cpu().numpy()
+    assert np.array_equal(bm, oracle.keys2block(keys.cpu().numpy()))
+
+
+def test_build_atomic_path_matches(dev, ab, oracle, monkeypatch):
+    monkeypatch.setenv("ADL_BLOOM_BUILD_ALGO", "atomic")
+    for n in (0, 5, 100_000):
+        keys = ab.synth_keys16(n, seed=5)
+        bm = ab.build(keys).cpu().numpy()
+        assert np.array_equal(bm, oracle.keys2block(keys.cpu().numpy().reshape(n, 16)))
+
+
+def test_build_duplicate_keys_hot_words(dev, ab, oracle):
+    # the collapsed-entropy hash concentrates bits; all-identical keys are the extreme
+    base = ab.synth_keys16(7, seed=1).cpu().numpy()
+    keys = np.repeat(base, 20000, axis=0)
+    bm = ab.build(to_dev(dev, keys)).cpu().numpy()
+    assert np.array_equal(bm, oracle.keys2block(keys))
+
+
+# ----------------------------------------------------------------- build, other key shapes
+@pytest.mark.parametrize("lo,hi,alpha", [(0, 40, None), (1, 300, None), (8, 8, None), (0, 3, None),
+                                         (3, 30, b"abcdefghij-0123456789")])
+def test_build_varlen_vs_oracle(dev, ab, oracle, lo, hi, alpha):
+    rng = random.Random(lo * 1000 + hi)
+    keys = rand_keys(rng, 7000, lo, hi, alpha)
+    dk, do, data, offs = packed_dev(dev, keys)
+    bm = ab.build(dk, do).cpu().numpy()
+    assert np.array_equal(bm, oracle.keys2block(data, offs))
+
+
+def test_build_synth_zipf_varlen(dev, ab, oracle):
+    data, offs = ab.synth_varlen(200_000, seed=0x5EED)
+    lens = (offs[1:] - offs[:-1]).cpu().numpy()
+    assert lens.min() >= 8 and lens.max() <= 256
+    assert 30 < lens.mean() < 50  # Zipf(1.1) over 8..256: mean ~40 B
+    bm = ab.build(data, offs).cpu().numpy()
+    h_off = offs.cpu().numpy().view(np.uint64)
+    assert np.array_equal(bm, oracle.keys2block(data.cpu().numpy(), h_off))
+
+
+@pytest.mark.parametrize("stride", [1, 4, 7, 9, 24, 32])
+def test_build_fixed_stride(dev, ab, oracle, stride):
+    rng = np.random.default_rng(stride)
+    keys = rng.integers(0, 256, size=(30000, stride), dtype=np.uint8)
+    bm = ab.build(to_dev(dev, keys)).cpu().numpy()
+    assert np.array_equal(bm, oracle.keys2block(keys))
+
+
+def test_build_unaligned_16b_keys(dev, ab, oracle):
+    # 16-byte keys at an odd address take the generic stride path
+    rng = np.random.default_rng(11)
+    keys = rng.integers(0, 256, size=(40000, 16), dtype=np.uint8)
+    buf = dev.zeros(40000 * 16 + 32, dtype=dev.uint8, device="cuda")
+    buf[1:1 + keys.size] = to_dev(dev, keys.reshape(-1))
+    view = buf[1:1 + keys.size].view(40000, 16)
+    bm = ab.build(view).cpu().numpy()
+    assert np.array_equal(bm, oracle.keys2block(keys))
+
+
+# ----------------------------------------------------------------- segmented (many SSTables)
+def test_build_segmented_vs_oracle(dev, ab, oracle):
+    sizes = [0, 1, 1000, 50_000, 7, 123_456, 6144, 6145, 3, 200_000, 10, 99_999, 2]
+    kb = np.concatenate([[0], np.cumsum(sizes)]).astype(np.uint64)
+    keys = ab.synth_keys16(int(kb[-1]), seed=42)
+    out, boff, nbytes = ab.build_segmented(keys, kb)
+    out = out.cpu().numpy()
+    hk = keys.cpu().numpy()
+    for f, n in enumerate(sizes):
+        want = oracle.keys2block(hk[kb[f]:kb[f + 1]])
+        got = out[int(boff[f]):int(boff[f]) + int(nbytes[f])]
+        assert np.array_equal(got, want), f
+
+
+def test_build_segmented_varlen(dev, ab, oracle):
+    rng = random.Random(8)
+    keys = rand_keys(rng, 20000, 0, 64)
+    dk, do, data, offs = packed_dev(dev, keys)
+    kb = np.array([0, 5000, 5001, 12000, 20000], dtype=np.uint64)
+    out, boff, nbytes = ab.build_segmented(dk, kb, offsets=do)
+    out = out.cpu().numpy()
+    for f in range(4):
+        sub = keys[int(kb[f]):int(kb[f + 1])]
+        got = out[int(boff[f]):int(boff[f]) + int(nbytes[f])]
+        assert np.array_equal(got, oracle.keys2block(sub)), f
+
+
+def test_build_compaction_shape_32_tables(dev, ab, oracle):
+    # 32 tables x 100k keys, seeds 0x5EED + t (scaled)
+    T, n = 32, 100_000
+    keys = dev.cat([ab.synth_keys16(n, seed=0x5EED + t) for t in range(T)])
+    kb = np.arange(T + 1, dtype=np.uint64) * n
+    out, boff, nbytes = ab.build_segmented(keys, kb)
+    out = out.cpu().numpy()
+    for t in (0, 1, 17, 31):
+        got = out[int(boff[t]):int(boff[t]) + int(nbytes[t])]
+        assert np.array_equal(got, oracle.keys2block(oracle.splitmix_keys16(0x5EED + t, n))), t
+
+
+# ----------------------------------------------------------------- probe
+def test_probe_matches_appendix_b(dev, ab, golden, oracle):
+    for g in golden["appendix_b"]["probes"]:
+        n = g["n"]
+        keys = ab.synth_keys16(n, seed=0x5EED)
+        bm = ab.build(keys)
+        assert bool(ab.probe(keys, bm).all().item())
+        q = ab.synth_keys16(n, seed=0x5EED, skip=n)
+        r = ab.probe(q, bm).cpu().numpy()
+        assert int(r.sum()) == g["false_positives"]
+        assert f"{sum(int(r[i]) << i for i in range(64)):016x}" == g["first64_mask_lsb_first"]
+        assert np.array_equal(r, oracle.probe(q.cpu().numpy(), bm.cpu().numpy()))
+
+
+def test_probe_varlen_and_bpk(dev, ab, oracle):
+    rng = random.Random(21)
+    ins = rand_keys(rng, 5000, 0, 50)
+    qry = rand_keys(rng, 20000, 0, 50) + ins[:100]
+    for bpk in (1, 4, 10, 23):
+        bm = oracle.keys2block(ins, bits_per_key=bpk)
+        dk, do, data, offs = packed_dev(dev, qry)
+        got = ab.probe(dk, to_dev(dev, bm), offsets=do, bits_per_key=bpk).cpu().numpy()
+        assert np.array_equal(got, oracle.probe(data, bm, offsets=offs, bits_per_key=bpk))
+
+
+def test_probe_multi_filters(dev, ab, oracle):
+    F, n = 9, 30000
+    sizes = [1000 * (f + 1) for f in range(F)]
+    bms = [oracle.keys2block(oracle.splitmix_keys16(100 + f, s)) for f, s in enumerate(sizes)]
+    boff = np.concatenate([[0], np.cumsum([b.size for b in bms])]).astype(np.uint64)
+    flat = np.concatenate(bms)
+    rng = np.random.default_rng(5)
+    fid = rng.integers(0, F + 2, size=n).astype(np.uint32)  # ids >= F answer 0
+    q = oracle.splitmix_keys16(104, n)
+    q[: n // 2] = oracle.splitmix_keys16(104, n // 2)  # half from filter 4's own keys
+    got = ab.probe_multi(to_dev(dev, q), to_dev(dev, fid), to_dev(dev, flat),
+                         to_dev(dev, boff.view(np.int64))).cpu().numpy()
+    want = oracle.probe_multi(q, fid, flat, boff)
+    assert np.array_equal(got, want)
+    assert not got[fid >= F].any()
+
+
+# ----------------------------------------------------------------- host API, C++ mirror
+def test_host_api_build_and_probe(dev, ab, oracle):
+    keys = oracle.splitmix_keys16(0x77, 33333)
+    bm = ab.build_host(keys)
+    assert np.array_equal(bm, oracle.keys2block(keys))
+    q = oracle.splitmix_keys16(0x78, 10000)
+    assert np.array_equal(ab.probe_host(q, bm), oracle.probe(q, bm))
+    empty = ab.build_host(np.zeros((0, 16), np.uint8))
+    assert empty.size == 7 and not empty.any()
+
+
+def test_filter_set_resident_probe(dev, ab, oracle):
+    bms = [oracle.keys2block(oracle.splitmix_keys16(200 + f, 5000 + f)) for f in range(4)]
+    boff = np.concatenate([[0], np.cumsum([b.size for b in bms])]).astype(np.uint64)
+    fs = ab.FilterSet(np.concatenate(bms), boff)
+    q = oracle.splitmix_keys16(201, 8000)
+    for f in range(4):
+        assert np.array_equal(fs.probe(q, filter=f), oracle.probe(q, bms[f])), f
+    assert not fs.probe(q, filter=7).any()
+    fid = (np.arange(8000) % 5).astype(np.uint32)
+    assert np.array_equal(fs.probe(q, filter_id=fid), oracle.probe_multi(q, fid, np.concatenate(bms), boff))
+    fs.close()
+
+
+def test_cpp_mirror_filter_block_test(dev, golden, oracle, tmp_path):
+    exe = os.path.join(ROOT, "adlsm-tree_amd", "bin", "filter_block_test")
+    out = tmp_path / "block.bin"
+    r = subprocess.run([exe, str(out)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    blk = out.read_bytes()
+    g = golden["appendix_b"]["filter_block_test"]
+    assert hashlib.sha256(blk).hexdigest() == g["sha256"]
+
+
+def test_errors_are_status_codes(dev, ab):
+    L = ab.lib()
+    # bits_per_key < 0 and a filter beyond the reference's int range
+    import ctypes
+
+    keys = ab.synth_keys16(16)
+    out = dev.empty(64, dtype=dev.uint8, device="cuda")
+    ws = dev.empty(1 << 20, dtype=dev.uint8, device="cuda")
+    st = ctypes.c_void_p(dev.cuda.current_stream().cuda_stream)
+    assert L.adl_bloom_build_device(keys.data_ptr(), None, 16, 16, -1, out.data_ptr(), ws.data_ptr(),
+                                    1 << 20, st) != 0
+    assert L.adl_bloom_build_device(keys.data_ptr(), None, 16, 16, 10, out.data_ptr(), ws.data_ptr(),
+                                    16, st) == -5  # workspace too small
+    assert L.adl_bloom_build_device(keys.data_ptr(), None, 2**31, 16, 10, out.data_ptr(), ws.data_ptr(),
+                                    1 << 20, st) == -2
+    assert L.adl_bloom_build_device(keys.data_ptr(), None, 16, 16, 10, out.data_ptr() + 1, ws.data_ptr(),
+                                    1 << 20, st) == -1  # misaligned bitmap
