@@ -273,6 +273,11 @@ __global__ __launch_bounds__(kBlockB) void bloom_tile_kernel(BuildArgs a,
 }
 
 // ---------------------------------------------------------------- direct atomics
+__global__ __launch_bounds__(256) void zero_kernel(uint4 *__restrict__ p, uint64_t n16) {
+  for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n16; i += (uint64_t)gridDim.x * 256)
+    p[i] = make_uint4(0, 0, 0, 0);
+}
+
 template <class Keys>
 __global__ __launch_bounds__(256) void bloom_atomic_kernel(Keys keys, uint64_t n, uint32_t k,
                                                            FastMod mod, uint32_t *__restrict__ bitmap) {
@@ -332,6 +337,16 @@ int make_plan(const uint64_t *counts, uint32_t nf, int32_t bpk, Plan &p) {
     const int v = atoi(e);
     if (v >= (int)kMinTileLog2 && v <= (int)kMaxTileLog2) TL = (uint32_t)v;
   }
+  // every filter's tile histogram must fit the LDS counters (T + 1 <= kHistMax)
+  auto max_tiles_at = [&](uint32_t tl) {
+    uint64_t t = 0;
+    for (uint32_t f = 0; f < nf; ++f) {
+      const uint64_t m = adl_host::bitmap_bytes(counts[f], bpk) * 8;
+      t = std::max<uint64_t>(t, (m + (1ull << tl) - 1) >> tl);
+    }
+    return t;
+  };
+  while (TL < kMaxTileLog2 && max_tiles_at(TL) + 1 > kHistMax) ++TL;
   p.a.nf = nf;
   p.a.k = k;
   p.a.C = C;
@@ -428,7 +443,10 @@ template <class Keys>
 int launch_atomic(const Plan &p, Keys keys, uint8_t *d_bitmaps, hipStream_t st) {
   for (uint32_t f = 0; f < p.a.nf; ++f) {
     const FilterDesc &d = p.a.f[f];
-    ADL_HIP_TRY(hipMemsetAsync(d_bitmaps + d.bitmap_off, 0, d.alloc_bytes, st));
+    const uint64_t n16 = d.alloc_bytes / 16;
+    hipLaunchKernelGGL(zero_kernel, dim3((uint32_t)std::min<uint64_t>((n16 + 255) / 256, 4096)), dim3(256), 0,
+                       st, reinterpret_cast<uint4 *>(d_bitmaps + d.bitmap_off), n16);
+    ADL_HIP_TRY(hipGetLastError());
     if (d.n == 0) continue;
     Keys kf = keys;
     const uint64_t blocks = std::min<uint64_t>((d.n + 255) / 256, 256 * 32);
@@ -569,39 +587,29 @@ int adl_bloom_build(const uint8_t *h_keys, const uint64_t *h_offsets, uint64_t n
     const uint64_t key_bytes = h_offsets ? (n ? h_offsets[n] : 0) : n * (uint64_t)key_stride;
     const uint64_t alloc = adl_host::round_up(bytes, 16);
     const uint64_t ws = adl_bloom_build_workspace_bytes(&n, 1, bits_per_key);
-    // one allocation: [keys | offsets | bitmap | workspace]
-    const uint64_t o_keys = 0;
+    const uint64_t off_bytes = h_offsets ? (n + 1) * 8 : 0;
+    // device: [keys | offsets | bitmap | workspace]; pinned host: [keys | offsets], then the bitmap
     const uint64_t o_offs = adl_host::round_up(key_bytes + 16, 256);
-    const uint64_t o_bm = o_offs + adl_host::round_up(h_offsets ? (n + 1) * 8 : 0, 256);
+    const uint64_t o_bm = o_offs + adl_host::round_up(off_bytes, 256);
     const uint64_t o_ws = o_bm + adl_host::round_up(alloc, 256);
-    const uint64_t total = o_ws + ws;
-    uint8_t *dev = nullptr;
-    ADL_HIP_TRY(hipMallocAsync((void **)&dev, total, st));
-    int rc = ADL_OK;
-    do {
-      if (key_bytes) {
-        if (hipMemcpyAsync(dev + o_keys, h_keys, key_bytes, hipMemcpyHostToDevice, st) != hipSuccess) {
-          rc = ADL_ERR_DEVICE;
-          break;
-        }
-      }
-      if (h_offsets) {
-        if (hipMemcpyAsync(dev + o_offs, h_offsets, (n + 1) * 8, hipMemcpyHostToDevice, st) != hipSuccess) {
-          rc = ADL_ERR_DEVICE;
-          break;
-        }
-      }
-      rc = adl_bloom_build_device(dev + o_keys, h_offsets ? reinterpret_cast<uint64_t *>(dev + o_offs) : nullptr,
-                                  n, key_stride, bits_per_key, dev + o_bm, dev + o_ws, ws, st);
-      if (rc) break;
-      if (hipMemcpyAsync(h_bitmap, dev + o_bm, bytes, hipMemcpyDeviceToHost, st) != hipSuccess) {
-        rc = ADL_ERR_DEVICE;
-        break;
-      }
-    } while (0);
-    (void)hipFreeAsync(dev, st);
-    if (hipStreamSynchronize(st) != hipSuccess && rc == ADL_OK) rc = ADL_ERR_DEVICE;
-    return rc;
+    adl_host::Staging &sg = adl_host::t_stage;
+    int rc = sg.reserve(std::max(o_bm, alloc), o_ws + ws);
+    if (rc) return rc;
+    if (key_bytes) memcpy(sg.host, h_keys, key_bytes);
+    if (off_bytes) memcpy(sg.host + o_offs, h_offsets, off_bytes);
+    if (o_bm && hipMemcpyAsync(sg.dev, sg.host, o_bm, hipMemcpyHostToDevice, st) != hipSuccess)
+      return ADL_ERR_DEVICE;
+    rc = adl_bloom_build_device(sg.dev, h_offsets ? reinterpret_cast<uint64_t *>(sg.dev + o_offs) : nullptr,
+                                n, key_stride, bits_per_key, sg.dev + o_bm, sg.dev + o_ws, ws, st);
+    if (rc) {
+      (void)hipStreamSynchronize(st);
+      return rc;
+    }
+    if (hipMemcpyAsync(sg.host, sg.dev + o_bm, bytes, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+      return ADL_ERR_DEVICE;
+    memcpy(h_bitmap, sg.host, bytes);
+    return ADL_OK;
   } catch (...) {
     return ADL_ERR_DEVICE;
   }

@@ -139,4 +139,40 @@ inline uint64_t bitmap_bytes(uint64_t n, int32_t bpk) {
 
 inline uint64_t round_up(uint64_t v, uint64_t a) { return (v + a - 1) / a * a; }
 
+// Per-thread staging for the synchronous host-pointer entry points: a pinned
+// host buffer (so every copy is a stream-ordered DMA; pageable hipMemcpyAsync
+// is not used anywhere) and a device buffer, both grown on demand and reused.
+// One per thread keeps the C-ABI re-entrant without locks.
+struct Staging {
+  uint8_t *host = nullptr;
+  uint64_t hcap = 0;
+  uint8_t *dev = nullptr;
+  uint64_t dcap = 0;
+  ~Staging() {
+    if (host) (void)hipHostFree(host);
+    if (dev) (void)hipFree(dev);
+  }
+  int reserve(uint64_t hbytes, uint64_t dbytes) {
+    if (hbytes > hcap) {
+      if (host) (void)hipHostFree(host);
+      host = nullptr;
+      hcap = 0;
+      const uint64_t want = round_up(hbytes + (hbytes >> 3), 1 << 16);
+      if (hipHostMalloc((void **)&host, want, hipHostMallocDefault) != hipSuccess) return ADL_ERR_OUT_OF_MEMORY;
+      hcap = want;
+    }
+    if (dbytes > dcap) {
+      if (dev) (void)hipFree(dev);
+      dev = nullptr;
+      dcap = 0;
+      const uint64_t want = round_up(dbytes + (dbytes >> 3), 1 << 16);
+      if (hipMalloc((void **)&dev, want) != hipSuccess) return ADL_ERR_OUT_OF_MEMORY;
+      dcap = want;
+    }
+    return ADL_OK;
+  }
+};
+
+inline thread_local Staging t_stage;
+
 }  // namespace adl_host

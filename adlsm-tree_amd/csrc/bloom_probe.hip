@@ -47,12 +47,12 @@ __global__ __launch_bounds__(kBlockP) void bloom_probe_kernel(Keys keys, uint64_
 // 32-bit `%` sequence instead of a launch-constant magic multiply.
 template <class Keys>
 __global__ __launch_bounds__(kBlockP) void bloom_probe_multi_kernel(
-    Keys keys, uint64_t n, uint32_t k, const uint32_t *__restrict__ fid, uint32_t nf,
-    const uint8_t *__restrict__ bitmaps, const uint64_t *__restrict__ boff,
+    Keys keys, uint64_t n, uint32_t k, const uint32_t *__restrict__ fid, uint32_t uniform_f,
+    uint32_t nf, const uint8_t *__restrict__ bitmaps, const uint64_t *__restrict__ boff,
     uint8_t *__restrict__ out) {
   for (uint64_t i = blockIdx.x * (uint64_t)kBlockP + threadIdx.x; i < n;
        i += (uint64_t)gridDim.x * kBlockP) {
-    const uint32_t f = fid[i];
+    const uint32_t f = fid ? fid[i] : uniform_f;  // fid == nullptr: every query -> uniform_f
     uint8_t hit = 0;
     if (f < nf) {
       const uint64_t b0 = boff[f], b1 = boff[f + 1];
@@ -183,6 +183,29 @@ int adl_bloom_probe_device(const uint8_t *d_keys, const uint64_t *d_offsets, uin
   });
 }
 
+}  // extern "C"
+
+namespace {
+// fid == nullptr sends every query to filter `uniform_f`.
+int probe_multi(const uint8_t *d_keys, const uint64_t *d_offsets, uint64_t n, uint32_t key_stride,
+                const uint32_t *d_filter_id, uint32_t uniform_f, uint32_t num_filters,
+                const uint8_t *d_bitmaps, const uint64_t *d_bitmap_off, int32_t bits_per_key,
+                uint8_t *d_out, hipStream_t st) {
+  if (num_filters && (!d_bitmaps || !d_bitmap_off)) return ADL_ERR_INVALID_ARG;
+  if (!d_offsets && key_stride == 0) return ADL_ERR_INVALID_ARG;
+  const uint32_t k = (uint32_t)adl_host::num_probes(bits_per_key);
+  return dispatch_keys(d_keys, d_offsets, key_stride, [&](auto keys) -> int {
+    hipLaunchKernelGGL(bloom_probe_multi_kernel<decltype(keys)>, dim3(grid_for(n, kBlockP)),
+                       dim3(kBlockP), 0, st, keys, n, k, d_filter_id, uniform_f, num_filters,
+                       d_bitmaps, d_bitmap_off, d_out);
+    ADL_HIP_TRY(hipGetLastError());
+    return ADL_OK;
+  });
+}
+}  // namespace
+
+extern "C" {
+
 int adl_bloom_probe_multi_device(const uint8_t *d_keys, const uint64_t *d_offsets, uint64_t n,
                                  uint32_t key_stride, const uint32_t *d_filter_id,
                                  uint32_t num_filters, const uint8_t *d_bitmaps,
@@ -190,17 +213,8 @@ int adl_bloom_probe_multi_device(const uint8_t *d_keys, const uint64_t *d_offset
                                  uint8_t *d_out, void *stream) {
   if (n == 0) return ADL_OK;
   if (!d_keys || !d_filter_id || !d_out || bits_per_key < 0) return ADL_ERR_INVALID_ARG;
-  if (num_filters && (!d_bitmaps || !d_bitmap_off)) return ADL_ERR_INVALID_ARG;
-  if (!d_offsets && key_stride == 0) return ADL_ERR_INVALID_ARG;
-  const uint32_t k = (uint32_t)adl_host::num_probes(bits_per_key);
-  hipStream_t st = (hipStream_t)stream;
-  return dispatch_keys(d_keys, d_offsets, key_stride, [&](auto keys) -> int {
-    hipLaunchKernelGGL(bloom_probe_multi_kernel<decltype(keys)>, dim3(grid_for(n, kBlockP)),
-                       dim3(kBlockP), 0, st, keys, n, k, d_filter_id, num_filters, d_bitmaps,
-                       d_bitmap_off, d_out);
-    ADL_HIP_TRY(hipGetLastError());
-    return ADL_OK;
-  });
+  return probe_multi(d_keys, d_offsets, n, key_stride, d_filter_id, 0, num_filters, d_bitmaps,
+                     d_bitmap_off, bits_per_key, d_out, (hipStream_t)stream);
 }
 
 int adl_bloom_probe(const uint8_t *h_keys, const uint64_t *h_offsets, uint64_t n,
@@ -211,29 +225,29 @@ int adl_bloom_probe(const uint8_t *h_keys, const uint64_t *h_offsets, uint64_t n
   if (!h_offsets && key_stride == 0) return ADL_ERR_INVALID_ARG;
   hipStream_t st = (hipStream_t)stream;
   const uint64_t key_bytes = h_offsets ? h_offsets[n] : n * (uint64_t)key_stride;
+  const uint64_t off_bytes = h_offsets ? (n + 1) * 8 : 0;
   const uint64_t o_offs = adl_host::round_up(key_bytes + 16, 256);
-  const uint64_t o_bm = o_offs + adl_host::round_up(h_offsets ? (n + 1) * 8 : 0, 256);
+  const uint64_t o_bm = o_offs + adl_host::round_up(off_bytes, 256);
   const uint64_t o_out = o_bm + adl_host::round_up(bitmap_bytes, 256);
   const uint64_t total = o_out + adl_host::round_up(n, 256);
-  uint8_t *dev = nullptr;
-  ADL_HIP_TRY(hipMallocAsync((void **)&dev, total, st));
-  int rc = ADL_OK;
-  do {
-    if (hipMemcpyAsync(dev, h_keys, key_bytes, hipMemcpyHostToDevice, st) != hipSuccess ||
-        (h_offsets && hipMemcpyAsync(dev + o_offs, h_offsets, (n + 1) * 8, hipMemcpyHostToDevice,
-                                     st) != hipSuccess) ||
-        hipMemcpyAsync(dev + o_bm, h_bitmap, bitmap_bytes, hipMemcpyHostToDevice, st) != hipSuccess) {
-      rc = ADL_ERR_DEVICE;
-      break;
-    }
-    rc = adl_bloom_probe_device(dev, h_offsets ? reinterpret_cast<uint64_t *>(dev + o_offs) : nullptr,
-                                n, key_stride, bits_per_key, dev + o_bm, bitmap_bytes, dev + o_out, st);
-    if (rc) break;
-    if (hipMemcpyAsync(h_out, dev + o_out, n, hipMemcpyDeviceToHost, st) != hipSuccess) rc = ADL_ERR_DEVICE;
-  } while (0);
-  (void)hipFreeAsync(dev, st);
-  if (hipStreamSynchronize(st) != hipSuccess && rc == ADL_OK) rc = ADL_ERR_DEVICE;
-  return rc;
+  adl_host::Staging &sg = adl_host::t_stage;
+  int rc = sg.reserve(o_out, total);
+  if (rc) return rc;
+  if (key_bytes) memcpy(sg.host, h_keys, key_bytes);
+  if (off_bytes) memcpy(sg.host + o_offs, h_offsets, off_bytes);
+  memcpy(sg.host + o_bm, h_bitmap, bitmap_bytes);
+  if (hipMemcpyAsync(sg.dev, sg.host, o_out, hipMemcpyHostToDevice, st) != hipSuccess) return ADL_ERR_DEVICE;
+  rc = adl_bloom_probe_device(sg.dev, h_offsets ? reinterpret_cast<uint64_t *>(sg.dev + o_offs) : nullptr, n,
+                              key_stride, bits_per_key, sg.dev + o_bm, bitmap_bytes, sg.dev + o_out, st);
+  if (rc) {
+    (void)hipStreamSynchronize(st);
+    return rc;
+  }
+  if (hipMemcpyAsync(sg.host, sg.dev + o_out, n, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess)
+    return ADL_ERR_DEVICE;
+  memcpy(h_out, sg.host, n);
+  return ADL_OK;
 }
 
 int adl_bloom_murmur3_device(const uint8_t *d_keys, const uint64_t *d_offsets, uint64_t n,
@@ -258,23 +272,21 @@ int adl_bloom_murmur3_device(const uint8_t *d_keys, const uint64_t *d_offsets, u
 
 int adl_bloom_murmur3(uint32_t seed, const void *data, uint64_t len, uint32_t *h_out) {
   if (!h_out || (len && !data) || len > 0xffffffffull) return ADL_ERR_INVALID_ARG;
-  uint8_t *dev = nullptr;
   const uint64_t o_out = adl_host::round_up(len + 16, 256);
-  ADL_HIP_TRY(hipMalloc((void **)&dev, o_out + 16));
-  int rc = ADL_OK;
-  uint32_t res[2] = {0, 0};
-  if ((len && hipMemcpy(dev, data, len, hipMemcpyHostToDevice) != hipSuccess)) rc = ADL_ERR_DEVICE;
-  if (rc == ADL_OK) {
-    hipLaunchKernelGGL(murmur3_seeded_kernel, dim3(1), dim3(kBlockP), 0, (hipStream_t)0, dev,
-                       (const uint64_t *)nullptr, (uint32_t)len, 1ull, seed, seed,
-                       reinterpret_cast<uint32_t *>(dev + o_out));
-    if (hipGetLastError() != hipSuccess ||
-        hipMemcpy(res, dev + o_out, 8, hipMemcpyDeviceToHost) != hipSuccess)
-      rc = ADL_ERR_DEVICE;
-  }
-  (void)hipFree(dev);
-  if (rc == ADL_OK) *h_out = res[0];
-  return rc;
+  adl_host::Staging &sg = adl_host::t_stage;
+  int rc = sg.reserve(o_out + 16, o_out + 16);
+  if (rc) return rc;
+  if (len) memcpy(sg.host, data, len);
+  hipStream_t st = nullptr;
+  if (len && hipMemcpyAsync(sg.dev, sg.host, len, hipMemcpyHostToDevice, st) != hipSuccess) return ADL_ERR_DEVICE;
+  hipLaunchKernelGGL(murmur3_seeded_kernel, dim3(1), dim3(kBlockP), 0, st, sg.dev, (const uint64_t *)nullptr,
+                     (uint32_t)len, 1ull, seed, seed, reinterpret_cast<uint32_t *>(sg.dev + o_out));
+  if (hipGetLastError() != hipSuccess ||
+      hipMemcpyAsync(sg.host + o_out, sg.dev + o_out, 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess)
+    return ADL_ERR_DEVICE;
+  memcpy(h_out, sg.host + o_out, 4);
+  return ADL_OK;
 }
 
 int adl_synth_keys16_device(uint8_t *d_out, uint64_t seed, uint64_t skip, uint64_t n, void *stream) {
@@ -357,32 +369,30 @@ int adl_bloom_filter_set_probe(const adl_bloom_filter_set *set, const uint8_t *h
   if (!h_keys || !h_out || (!h_offsets && key_stride == 0)) return ADL_ERR_INVALID_ARG;
   hipStream_t st = (hipStream_t)stream;
   const uint64_t key_bytes = h_offsets ? h_offsets[n] : n * (uint64_t)key_stride;
+  const uint64_t off_bytes = h_offsets ? (n + 1) * 8 : 0;
   const uint64_t o_offs = adl_host::round_up(key_bytes + 16, 256);
-  const uint64_t o_fid = o_offs + adl_host::round_up(h_offsets ? (n + 1) * 8 : 0, 256);
-  const uint64_t o_out = o_fid + adl_host::round_up(n * 4, 256);
+  const uint64_t o_fid = o_offs + adl_host::round_up(off_bytes, 256);
+  const uint64_t o_out = o_fid + adl_host::round_up(h_filter_id ? n * 4 : 0, 256);
   const uint64_t total = o_out + adl_host::round_up(n, 256);
-  uint8_t *dev = nullptr;
-  ADL_HIP_TRY(hipMallocAsync((void **)&dev, total, st));
-  int rc = ADL_OK;
-  do {
-    uint32_t *d_fid = reinterpret_cast<uint32_t *>(dev + o_fid);
-    if ((key_bytes && hipMemcpyAsync(dev, h_keys, key_bytes, hipMemcpyHostToDevice, st) != hipSuccess) ||
-        (h_offsets && hipMemcpyAsync(dev + o_offs, h_offsets, (n + 1) * 8, hipMemcpyHostToDevice,
-                                     st) != hipSuccess) ||
-        (h_filter_id && hipMemcpyAsync(d_fid, h_filter_id, n * 4, hipMemcpyHostToDevice, st) != hipSuccess) ||
-        (!h_filter_id && hipMemsetD32Async((hipDeviceptr_t)d_fid, (int)filter, n, st) != hipSuccess)) {
-      rc = ADL_ERR_DEVICE;
-      break;
-    }
-    rc = adl_bloom_probe_multi_device(dev, h_offsets ? reinterpret_cast<uint64_t *>(dev + o_offs) : nullptr,
-                                      n, key_stride, d_fid, set->nf, set->d_bitmaps, set->d_off,
-                                      set->bpk, dev + o_out, st);
-    if (rc) break;
-    if (hipMemcpyAsync(h_out, dev + o_out, n, hipMemcpyDeviceToHost, st) != hipSuccess) rc = ADL_ERR_DEVICE;
-  } while (0);
-  (void)hipFreeAsync(dev, st);
-  if (hipStreamSynchronize(st) != hipSuccess && rc == ADL_OK) rc = ADL_ERR_DEVICE;
-  return rc;
+  adl_host::Staging &sg = adl_host::t_stage;
+  int rc = sg.reserve(o_out, total);
+  if (rc) return rc;
+  if (key_bytes) memcpy(sg.host, h_keys, key_bytes);
+  if (off_bytes) memcpy(sg.host + o_offs, h_offsets, off_bytes);
+  if (h_filter_id) memcpy(sg.host + o_fid, h_filter_id, n * 4);
+  if (hipMemcpyAsync(sg.dev, sg.host, o_out, hipMemcpyHostToDevice, st) != hipSuccess) return ADL_ERR_DEVICE;
+  rc = probe_multi(sg.dev, h_offsets ? reinterpret_cast<uint64_t *>(sg.dev + o_offs) : nullptr, n, key_stride,
+                   h_filter_id ? reinterpret_cast<uint32_t *>(sg.dev + o_fid) : nullptr, filter, set->nf,
+                   set->d_bitmaps, set->d_off, set->bpk, sg.dev + o_out, st);
+  if (rc) {
+    (void)hipStreamSynchronize(st);
+    return rc;
+  }
+  if (hipMemcpyAsync(sg.host, sg.dev + o_out, n, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess)
+    return ADL_ERR_DEVICE;
+  memcpy(h_out, sg.host, n);
+  return ADL_OK;
 }
 
 int adl_bloom_filter_set_device_view(const adl_bloom_filter_set *set, const uint8_t **d_bitmaps,

@@ -35,6 +35,9 @@ int main(int argc, char **argv) {
   std::string block;
   CHECK(writer.Final(block) == OK);
   CHECK(block.size() == 100111u);
+  if (argc > 1) {
+    std::ofstream(argv[1], std::ios::binary).write(block.data(), (std::streamsize)block.size());
+  }
 
   FilterBlockReader reader;
   CHECK(reader.Init(block) == OK);
@@ -54,6 +57,31 @@ int main(int argc, char **argv) {
   int positives = 0;
   for (uint8_t h : hits) positives += h;
   CHECK(positives == 10000);
+  if (positives != 10000) {
+    int shown = 0;
+    for (int i = 0; i < 10000 && shown < 8; ++i) {
+      if (!hits[i]) {
+        const std::string k = "hello-ddl" + std::to_string(i);
+        fprintf(stderr, "  batch miss %d (%s): single-key probe says %d\n", i, k.c_str(),
+                (int)reader.IsKeyExists(0, k));
+        ++shown;
+      }
+    }
+    fprintf(stderr, "  batch positives %d / 10000\n", positives);
+    // diagnostics: growing prefixes of the batch, and the host-bitmap API
+    for (int len : {1, 2, 3, 4, 8, 16, 64, 256, 1000}) {
+      KeyArena part;
+      for (int i = 0; i < len; ++i) part.Add("hello-ddl" + std::to_string(i));
+      std::vector<uint8_t> ph;
+      RC rc = reader.IsKeysExist(0, part, ph);
+      int pp = 0;
+      for (uint8_t h : ph) pp += h;
+      fprintf(stderr, "  prefix %d: rc=%d positives=%d\n", len, (int)rc, pp);
+    }
+    fprintf(stderr, "  arena bytes=%zu offsets[0..3]=%lu %lu %lu last=%lu\n", batch.bytes().size(),
+            (unsigned long)batch.offsets()[0], (unsigned long)batch.offsets()[1],
+            (unsigned long)batch.offsets()[2], (unsigned long)batch.offsets().back());
+  }
   CHECK(reader.IsKeyExists(1, "adl"));
   CHECK(reader.IsKeyExists(1, "dont"));
   CHECK(reader.IsKeyExists(1, "like-apple"));
@@ -80,9 +108,6 @@ int main(int argc, char **argv) {
   wrong_type[wrong_type.size() - 11] = 'x';  // "bf:" -> "xf:"
   CHECK(bad.Init(wrong_type) == FILTER_BLOCK_ERROR);
 
-  if (argc > 1) {
-    std::ofstream(argv[1], std::ios::binary).write(block.data(), (std::streamsize)block.size());
-  }
   if (g_failures) {
     fprintf(stderr, "filter_block_test: %d check(s) failed\n", g_failures);
     return 1;

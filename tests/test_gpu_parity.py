@@ -142,8 +142,20 @@ def test_build_atomic_path_matches(dev, ab, oracle, monkeypatch):
     monkeypatch.setenv("ADL_BLOOM_BUILD_ALGO", "atomic")
     for n in (0, 5, 100_000):
         keys = ab.synth_keys16(n, seed=5)
-        bm = ab.build(keys).cpu().numpy()
+        b = ab.Builder(n, 10)
+        b.bitmap.fill_(0xA5)  # the build must not rely on a pre-zeroed bitmap
+        bm = b.build(keys).cpu().numpy()
         assert np.array_equal(bm, oracle.keys2block(keys.cpu().numpy().reshape(n, 16)))
+
+
+def test_build_binned_overwrites_dirty_bitmap(dev, ab, oracle):
+    keys = ab.synth_keys16(77_777, seed=6)
+    b = ab.Builder(77_777, 10)
+    b.bitmap.fill_(0xFF)
+    b.ws.fill_(0x5A)
+    bm = b.build(keys).cpu().numpy()
+    assert np.array_equal(bm, oracle.keys2block(keys.cpu().numpy()))
+    assert not b.bitmap[b.nbytes:].any().item()  # 16-byte pad written as zero
 
 
 def test_build_duplicate_keys_hot_words(dev, ab, oracle):
@@ -299,14 +311,42 @@ def test_filter_set_resident_probe(dev, ab, oracle):
     fs.close()
 
 
+def test_host_api_varlen(dev, ab, oracle):
+    rng = random.Random(77)
+    keys = [b"hello-ddl%d" % i for i in range(10000)] + rand_keys(rng, 3000, 0, 70)
+    data, offs = oracle.pack(keys)
+    bm = ab.build_host(data, offs)
+    assert np.array_equal(bm, oracle.keys2block(data, offs))
+    assert ab.probe_host(data, bm, offsets=offs).all()
+    q = rand_keys(rng, 5000, 0, 70)
+    qd, qo = oracle.pack(q)
+    assert np.array_equal(ab.probe_host(qd, bm, offsets=qo), oracle.probe(qd, bm, offsets=qo))
+
+
+def test_filter_set_varlen(dev, ab, oracle):
+    rng = random.Random(78)
+    b0 = [b"hello", b"world", b"hello-yly", b"hello-ddl"] + [b"hello-ddl%d" % i for i in range(10000)]
+    b1 = [b"adl", b"dont", b"like-apple"]
+    bms = [oracle.keys2block(b0), oracle.keys2block(b1)]
+    boff = np.array([0, bms[0].size, bms[0].size + bms[1].size], dtype=np.uint64)
+    fs = ab.FilterSet(np.concatenate(bms), boff)
+    d0, o0 = oracle.pack(b0)
+    assert fs.probe(d0, filter=0, offsets=o0).all()
+    q = rand_keys(rng, 4000, 0, 30)
+    qd, qo = oracle.pack(q)
+    assert np.array_equal(fs.probe(qd, filter=0, offsets=qo), oracle.probe(qd, bms[0], offsets=qo))
+    assert np.array_equal(fs.probe(qd, filter=1, offsets=qo), oracle.probe(qd, bms[1], offsets=qo))
+    fs.close()
+
+
 def test_cpp_mirror_filter_block_test(dev, golden, oracle, tmp_path):
     exe = os.path.join(ROOT, "adlsm-tree_amd", "bin", "filter_block_test")
     out = tmp_path / "block.bin"
     r = subprocess.run([exe, str(out)], capture_output=True, text=True, timeout=300)
-    assert r.returncode == 0, r.stdout + r.stderr
     blk = out.read_bytes()
     g = golden["appendix_b"]["filter_block_test"]
-    assert hashlib.sha256(blk).hexdigest() == g["sha256"]
+    assert hashlib.sha256(blk).hexdigest() == g["sha256"], "mirror's filter block differs from the reference"
+    assert r.returncode == 0, r.stdout + r.stderr
 
 
 def test_errors_are_status_codes(dev, ab):
