@@ -41,7 +41,8 @@ namespace {
 constexpr int kBlockA = 1024;       // pass A threads per workgroup (16 waves)
 constexpr int kKptMax = 8;          // keys per thread, pass A
 constexpr int kBlockB = 1024;       // pass B threads per workgroup
-constexpr int kUnrollB = 8;         // gathered positions in flight per lane, pass B
+constexpr int kDepth = 8;           // segments per pipeline stage per wave, pass B (2 stages)
+constexpr int kSegBatch = 2048;     // segments staged in LDS per batch, pass B
 constexpr int kMaxFilters = 8;      // filters per launch pair (descriptors ride in kernargs)
 constexpr uint32_t kHistMax = 2049; // tiles per filter + 1 (m < 2^31, TL >= ... keeps T <= 2048)
 constexpr uint32_t kPosLdsWords = 36864;  // 144 KiB of sorted positions per chunk
@@ -68,6 +69,7 @@ struct BuildArgs {
   uint32_t k;      // probes per key
   uint32_t C;      // keys per chunk
   uint32_t TL;     // log2 tile bits
+  uint32_t xcd_remap;  // pass A: consecutive chunks on one XCD (tuning, ADL_BLOOM_XCD_REMAP)
   FilterDesc f[kMaxFilters];
 };
 
@@ -88,188 +90,306 @@ __device__ __forceinline__ int find_filter_by_tile(const BuildArgs &a, uint32_t 
 }
 
 // ---------------------------------------------------------------- pass A
+// Register prefetch of a chunk's keys.  Only the fixed 16-byte view has raw
+// words worth holding (4 VGPRs per key); the other views hash straight from
+// memory.
+template <class Keys>
+struct KeyRegs {
+  static constexpr bool kPrefetch = false;
+  uint32_t dummy;
+};
+template <>
+struct KeyRegs<Keys16> {
+  static constexpr bool kPrefetch = true;
+  uint4 raw;
+};
+
+// Persistent: workgroup b processes chunks b, b + gridDim.x, ...  While chunk c
+// is hashed, sorted and stored, the keys of the next chunk are already in
+// flight into registers, so the key stream overlaps the LDS work and the
+// sorted-chunk stores drain behind the next chunk's hashing.
+//
 // KFIX > 0: k known at compile time, positions kept in registers between the
 // count and the scatter; KFIX == 0: runtime k, positions recomputed.
-template <int KFIX, class Keys>
+template <int KFIX, int KPT, class Keys>
 __global__ __launch_bounds__(kBlockA) void bloom_bin_kernel(BuildArgs a, Keys keys,
                                                             uint32_t *__restrict__ pos_ws,
-                                                            uint32_t *__restrict__ table_ws) {
+                                                            uint32_t *__restrict__ table_ws,
+                                                            uint32_t total_chunks) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   const int tid = threadIdx.x;
-  const uint32_t wg = blockIdx.x;
-  const int fi = find_filter_by_chunk(a, wg);
-  const FilterDesc &d = a.f[fi];
-  const uint32_t w = wg - d.chunk_base;
   const uint32_t C = a.C;
   const uint32_t k = KFIX > 0 ? (uint32_t)KFIX : a.k;
   const uint32_t TL = a.TL;
-  const uint32_t first = w * C;
-  const uint32_t cnt = min(C, d.n - first);
-  const uint32_t T = d.tiles;
   const uint32_t hist_words = (kHistMax + 3) & ~3u;
   uint32_t *hist = lds;                       // T+1 counters, later cursors
   uint32_t *scratch = lds + hist_words;       // scan scratch (BLOCK/64 + 1, padded to 32)
   uint32_t *lpos = lds + hist_words + 32;     // k*C sorted positions
-  const FastMod mod = d.mod;
+  constexpr bool PF = KeyRegs<Keys>::kPrefetch;
 
-  for (uint32_t i = tid; i <= T; i += kBlockA) hist[i] = 0;
+  auto fetch = [&](uint32_t chunk, KeyRegs<Keys> (&r)[KPT]) {
+    if constexpr (PF) {
+      const FilterDesc &d = a.f[find_filter_by_chunk(a, chunk)];
+      const uint32_t first = (chunk - d.chunk_base) * C;
+      const uint32_t cnt = min(C, d.n - first);
+#pragma unroll
+      for (int i = 0; i < KPT; ++i) {
+        const uint32_t idx = tid + i * kBlockA;
+        if (idx < cnt) r[i].raw = keys.keys[d.key_begin + first + idx];
+      }
+    }
+  };
 
-  uint32_t h1[kKptMax], h2[kKptMax];
-#pragma unroll
-  for (int i = 0; i < kKptMax; ++i) {
-    const uint32_t idx = tid + i * kBlockA;
-    h1[i] = h2[i] = 0;
-    if (idx < cnt) keys.hash(d.key_begin + first + idx, h1[i], h2[i]);
-  }
-  __syncthreads();
+  // Round r of the persistent grid covers chunks [r*G, (r+1)*G).  Inside a
+  // round, the 8 XCDs (blocks b, b+8, ... share one under round-robin
+  // dispatch) each take G/8 consecutive chunks, so the 4-byte (tile, chunk)
+  // table entries of neighbouring chunks -- one 64-byte line holds 16 -- are
+  // written from one L2 and leave it as whole lines.  Speed only: any
+  // placement gives the same result.
+  const uint32_t G = gridDim.x;
+  const uint32_t slot =
+      (a.xcd_remap && G % 8 == 0) ? (blockIdx.x % 8) * (G / 8) + blockIdx.x / 8 : blockIdx.x;
+  const uint32_t rounds = (total_chunks + G - 1) / G;
+  KeyRegs<Keys> cur[KPT];
+  if (slot < total_chunks) fetch(slot, cur);
+  for (uint32_t i = tid; i < kHistMax; i += kBlockA) hist[i] = 0;
 
-  constexpr int KR = KFIX > 0 ? KFIX : 1;
-  uint32_t pos[kKptMax][KR];
+  for (uint32_t r = 0; r < rounds; ++r) {
+    const uint32_t wg = r * G + slot;
+    if (wg >= total_chunks) break;  // only the last round is partial
+    const int fi = find_filter_by_chunk(a, wg);
+    const FilterDesc &d = a.f[fi];
+    const uint32_t w = wg - d.chunk_base;
+    const uint32_t first = w * C;
+    const uint32_t cnt = min(C, d.n - first);
+    const uint32_t T = d.tiles;
+    const FastMod mod = d.mod;
+
+    KeyRegs<Keys> nxt[KPT];
+    if (wg + G < total_chunks) fetch(wg + G, nxt);
+
+    uint32_t h1[KPT], h2[KPT];
 #pragma unroll
-  for (int i = 0; i < kKptMax; ++i) {
-    const uint32_t idx = tid + i * kBlockA;
-    if (idx < cnt) {
-      if constexpr (KFIX > 0) {
+    for (int i = 0; i < KPT; ++i) {
+      const uint32_t idx = tid + i * kBlockA;
+      h1[i] = h2[i] = 0;
+      if (idx < cnt) {
+        if constexpr (PF) hash16(cur[i].raw, h1[i], h2[i]);
+        else keys.hash(d.key_begin + first + idx, h1[i], h2[i]);
+      }
+    }
+    __syncthreads();  // hist cleared (previous iteration / prologue)
+
+    constexpr int KR = KFIX > 0 ? KFIX : 1;
+    uint32_t pos[KPT][KR];
 #pragma unroll
-        for (int j = 0; j < KFIX; ++j) {
-          pos[i][j] = fastmod(h1[i] + (uint32_t)j * h2[i], mod);
-          atomicAdd(&hist[pos[i][j] >> TL], 1u);
-        }
-      } else {
-        for (uint32_t j = 0; j < k; ++j) {
-          const uint32_t p = fastmod(h1[i] + j * h2[i], mod);
-          atomicAdd(&hist[p >> TL], 1u);
+    for (int i = 0; i < KPT; ++i) {
+      const uint32_t idx = tid + i * kBlockA;
+      if (idx < cnt) {
+        if constexpr (KFIX > 0) {
+#pragma unroll
+          for (int j = 0; j < KFIX; ++j) {
+            pos[i][j] = fastmod(h1[i] + (uint32_t)j * h2[i], mod);
+            atomicAdd(&hist[pos[i][j] >> TL], 1u);
+          }
+        } else {
+          for (uint32_t j = 0; j < k; ++j) {
+            const uint32_t p = fastmod(h1[i] + j * h2[i], mod);
+            atomicAdd(&hist[p >> TL], 1u);
+          }
         }
       }
     }
-  }
-  __syncthreads();
+    __syncthreads();
 
-  // Exclusive scan: hist[t] = start of tile t's run; hist[T] = k*cnt.
-  block_excl_scan_array<kBlockA>(hist, T + 1, scratch);
+    // Exclusive scan: hist[t] = start of tile t's run; hist[T] = k*cnt.
+    block_excl_scan_array<kBlockA>(hist, T + 1, scratch);
 
-  // (tile, chunk) table, T+1 rows of W entries: row t = start of tile t.
-  uint32_t *tab = table_ws + d.table_base;
-  for (uint32_t t = tid; t <= T; t += kBlockA) tab[(uint64_t)t * d.chunks + w] = hist[t];
-  __syncthreads();
+    // (tile, chunk) table, T+1 rows of W entries: row t = start of tile t.
+    uint32_t *tab = table_ws + d.table_base;
+    for (uint32_t t = tid; t <= T; t += kBlockA) tab[(uint64_t)t * d.chunks + w] = hist[t];
+    __syncthreads();
 
-  // Scatter into LDS by tile (hist now serves as the per-tile cursor).
+    // Scatter into LDS by tile (hist now serves as the per-tile cursor).
 #pragma unroll
-  for (int i = 0; i < kKptMax; ++i) {
-    const uint32_t idx = tid + i * kBlockA;
-    if (idx < cnt) {
-      if constexpr (KFIX > 0) {
+    for (int i = 0; i < KPT; ++i) {
+      const uint32_t idx = tid + i * kBlockA;
+      if (idx < cnt) {
+        if constexpr (KFIX > 0) {
 #pragma unroll
-        for (int j = 0; j < KFIX; ++j) {
-          const uint32_t slot = atomicAdd(&hist[pos[i][j] >> TL], 1u);
-          lpos[slot] = pos[i][j];
-        }
-      } else {
-        for (uint32_t j = 0; j < k; ++j) {
-          const uint32_t p = fastmod(h1[i] + j * h2[i], mod);
-          const uint32_t slot = atomicAdd(&hist[p >> TL], 1u);
-          lpos[slot] = p;
+          for (int j = 0; j < KFIX; ++j) {
+            const uint32_t slot = atomicAdd(&hist[pos[i][j] >> TL], 1u);
+            lpos[slot] = pos[i][j];
+          }
+        } else {
+          for (uint32_t j = 0; j < k; ++j) {
+            const uint32_t p = fastmod(h1[i] + j * h2[i], mod);
+            const uint32_t slot = atomicAdd(&hist[p >> TL], 1u);
+            lpos[slot] = p;
+          }
         }
       }
     }
-  }
-  __syncthreads();
+    __syncthreads();
 
-  // Stream the sorted chunk out: k*cnt words, region w is k*C words long
-  // (16-byte aligned because C % 4 == 0 and pos_base % 4 == 0).
-  const uint32_t total = k * cnt;
-  uint32_t *dst = pos_ws + d.pos_base + (uint64_t)w * k * C;
-  const uint32_t nvec = total >> 2;
-  const uint4 *src4 = reinterpret_cast<const uint4 *>(lpos);
-  uint4 *dst4 = reinterpret_cast<uint4 *>(dst);
-  for (uint32_t i = tid; i < nvec; i += kBlockA) dst4[i] = src4[i];
-  for (uint32_t i = (nvec << 2) + tid; i < total; i += kBlockA) dst[i] = lpos[i];
+    // Stream the sorted chunk out: k*cnt words, region w is k*C words long
+    // (16-byte aligned because C % 4 == 0 and pos_base % 4 == 0).  The hist
+    // is cleared for the next chunk meanwhile (the scatter is done with it).
+    for (uint32_t i = tid; i <= T; i += kBlockA) hist[i] = 0;
+    const uint32_t total = k * cnt;
+    uint32_t *dst = pos_ws + d.pos_base + (uint64_t)w * k * C;
+    const uint32_t nvec = total >> 2;
+    const uint4 *src4 = reinterpret_cast<const uint4 *>(lpos);
+    uint4 *dst4 = reinterpret_cast<uint4 *>(dst);
+    for (uint32_t i = tid; i < nvec; i += kBlockA) dst4[i] = src4[i];
+    for (uint32_t i = (nvec << 2) + tid; i < total; i += kBlockA) dst[i] = lpos[i];
+
+    if constexpr (PF) {
+#pragma unroll
+      for (int i = 0; i < KPT; ++i) cur[i] = nxt[i];
+    }
+  }
 }
 
 // ---------------------------------------------------------------- pass B
+// Persistent: workgroup b owns tiles b, b + gridDim.x, ...  For a tile, the
+// (tile, chunk) table rows give one segment per chunk region.  A wave takes
+// whole segments (segment j -> wave j % 16) and reads up to 2 x 64 positions
+// of each with two predicated wave-loads (no per-element search), through a
+// two-stage register pipeline: the loads of the next kDepth segments are in
+// flight while the current kDepth are ds_or_b32'd into the LDS tile.  The next
+// tile's table rows are prefetched into registers during the gather, and the
+// finished tile's 16-byte stores drain while the next tile starts.
+template <int DEPTH>
+struct SegStage {
+  uint32_t v0[DEPTH], v1[DEPTH];
+};
+
 __global__ __launch_bounds__(kBlockB) void bloom_tile_kernel(BuildArgs a,
                                                              const uint32_t *__restrict__ pos_ws,
                                                              const uint32_t *__restrict__ table_ws,
-                                                             uint8_t *__restrict__ bitmaps) {
+                                                             uint8_t *__restrict__ bitmaps,
+                                                             uint32_t total_tiles) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   const int tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid / kWave;
   constexpr int NWAVES = kBlockB / kWave;
-  const uint32_t wg = blockIdx.x;
-  const int fi = find_filter_by_tile(a, wg);
-  const FilterDesc &d = a.f[fi];
-  const uint32_t lt = wg - d.tile_base;
+  constexpr int RPT = kSegBatch / kBlockB;  // table entries per thread per batch
   const uint32_t TL = a.TL;
   const uint32_t tile_words = 1u << (TL - 5);
   const uint32_t tmask = (1u << TL) - 1u;
-  const uint32_t W = d.chunks;
-  const uint32_t k = a.k;
-  const uint32_t region = k * a.C;
+  const uint32_t region = a.k * a.C;
+  uint32_t *tile = lds;                    // 2^TL bits
+  uint32_t *sbase = lds + tile_words;      // kSegBatch segment start words
+  uint32_t *slen = sbase + kSegBatch;      // kSegBatch segment lengths
 
-  uint32_t *tile = lds;                          // 2^TL bits
-  uint32_t *vstart = lds + tile_words;           // kBlockB + 1 virtual starts
-  uint32_t *segbase = vstart + kBlockB + 4;      // kBlockB segment bases (u32, wrapping)
-  uint32_t *scratch = segbase + kBlockB;         // scan scratch
-
-  for (uint32_t i = tid; i < tile_words; i += kBlockB) tile[i] = 0;
-
-  const uint32_t *row0 = table_ws + d.table_base + (uint64_t)lt * W;
-  const uint32_t *row1 = row0 + W;
-  const uint32_t pos_base = (uint32_t)d.pos_base;
-
-  for (uint32_t wb = 0; wb < W; wb += kBlockB) {
-    const uint32_t nw = min((uint32_t)kBlockB, W - wb);
-    uint32_t s = 0, len = 0;
-    if ((uint32_t)tid < nw) {
-      s = row0[wb + tid];
-      len = row1[wb + tid] - s;
-    }
-    uint32_t L;
-    const uint32_t vs = block_excl_scan<kBlockB>(len, scratch, &L);
-    if ((uint32_t)tid < nw) {
-      vstart[tid] = vs;
-      segbase[tid] = pos_base + (wb + tid) * region + s - vs;  // address = segbase[w] + e
-    }
-    if (tid == 0) vstart[nw] = L;
-    __syncthreads();
-
-    for (uint32_t base = wave * kWave * kUnrollB; base < L; base += NWAVES * kWave * kUnrollB) {
-      const uint32_t e0 = base + lane;
-      uint32_t lo = 0, hi = nw;  // vstart[lo] <= e0 < vstart[hi]
-      while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (vstart[mid] <= e0) lo = mid; else hi = mid;
-      }
-      uint32_t wseg = lo;
-      uint32_t v[kUnrollB];
+  auto fetch_rows = [&](uint32_t wg, uint32_t wb, uint32_t (&rs)[RPT], uint32_t (&re)[RPT]) {
+    const FilterDesc &d = a.f[find_filter_by_tile(a, wg)];
+    const uint32_t lt = wg - d.tile_base, W = d.chunks;
+    const uint32_t *row0 = table_ws + d.table_base + (uint64_t)lt * W;
 #pragma unroll
-      for (int u = 0; u < kUnrollB; ++u) {
-        const uint32_t e = e0 + u * kWave;
-        v[u] = 0xffffffffu;
-        if (e < L) {
-          while (vstart[wseg + 1] <= e) ++wseg;
-          v[u] = pos_ws[segbase[wseg] + e];
+    for (int r = 0; r < RPT; ++r) {
+      const uint32_t i = wb + tid + r * kBlockB;
+      rs[r] = re[r] = 0;
+      if (i < W && (uint32_t)(tid + r * kBlockB) < (uint32_t)kSegBatch) {
+        rs[r] = row0[i];
+        re[r] = row0[i + W];
+      }
+    }
+  };
+
+  auto or_pos = [&](uint32_t v) {
+    const uint32_t off = v & tmask;
+    atomicOr(&tile[off >> 5], 1u << (off & 31));
+  };
+
+  uint32_t pre_s[RPT], pre_e[RPT];
+  if (blockIdx.x < total_tiles) fetch_rows(blockIdx.x, 0, pre_s, pre_e);
+
+  for (uint32_t wg = blockIdx.x; wg < total_tiles; wg += gridDim.x) {
+    const int fi = find_filter_by_tile(a, wg);
+    const FilterDesc &d = a.f[fi];
+    const uint32_t lt = wg - d.tile_base;
+    const uint32_t W = d.chunks;
+    const uint32_t pos_base = (uint32_t)d.pos_base;
+
+    uint4 *t4w = reinterpret_cast<uint4 *>(tile);
+    for (uint32_t i = tid; i < tile_words / 4; i += kBlockB) t4w[i] = make_uint4(0, 0, 0, 0);
+    // an empty filter (no chunks) has no batch to prefetch the next tile from
+    if (W == 0 && wg + gridDim.x < total_tiles) fetch_rows(wg + gridDim.x, 0, pre_s, pre_e);
+    __syncthreads();  // tile zeroed (also when W == 0)
+
+    for (uint32_t wb = 0; wb < W; wb += kSegBatch) {
+      const uint32_t nw = min((uint32_t)kSegBatch, W - wb);
+      uint32_t rs[RPT], re[RPT];
+      if (wb == 0) {
+#pragma unroll
+        for (int r = 0; r < RPT; ++r) rs[r] = pre_s[r], re[r] = pre_e[r];
+      } else {
+        fetch_rows(wg, wb, rs, re);
+      }
+#pragma unroll
+      for (int r = 0; r < RPT; ++r) {
+        const uint32_t i = tid + r * kBlockB;
+        if (i < nw) {
+          sbase[i] = pos_base + (wb + i) * region + rs[r];
+          slen[i] = re[r] - rs[r];
         }
       }
+      __syncthreads();  // segment list ready (and the tile zeroed)
+      if (wb + kSegBatch >= W && wg + gridDim.x < total_tiles) fetch_rows(wg + gridDim.x, 0, pre_s, pre_e);
+
+      // this wave's segments: j = wave + NWAVES * q, q < Q
+      const uint32_t Q = nw > (uint32_t)wave ? (nw - wave + NWAVES - 1) / NWAVES : 0;
+      auto issue = [&](SegStage<kDepth> &st, uint32_t q0) {
 #pragma unroll
-      for (int u = 0; u < kUnrollB; ++u) {
-        const uint32_t e = e0 + u * kWave;
-        if (e < L) {
-          const uint32_t off = v[u] & tmask;
-          atomicOr(&tile[off >> 5], 1u << (off & 31));
+        for (int u = 0; u < kDepth; ++u) {
+          const uint32_t q = q0 + u;
+          st.v0[u] = st.v1[u] = 0;
+          if (q < Q) {
+            const uint32_t j = wave + NWAVES * q;
+            const uint32_t len = slen[j], b = sbase[j];
+            if ((uint32_t)lane < len) st.v0[u] = pos_ws[b + lane];
+            if ((uint32_t)lane + kWave < len) st.v1[u] = pos_ws[b + kWave + lane];
+          }
         }
+      };
+      auto consume = [&](const SegStage<kDepth> &st, uint32_t q0) {
+#pragma unroll
+        for (int u = 0; u < kDepth; ++u) {
+          const uint32_t q = q0 + u;
+          if (q < Q) {
+            const uint32_t j = wave + NWAVES * q;
+            const uint32_t len = slen[j];
+            if ((uint32_t)lane < len) or_pos(st.v0[u]);
+            if ((uint32_t)lane + kWave < len) or_pos(st.v1[u]);
+            if (len > 2u * kWave) {  // rare: long segments of hot tiles
+              const uint32_t b = sbase[j];
+              for (uint32_t o = 2 * kWave + lane; o < len; o += kWave) or_pos(pos_ws[b + o]);
+            }
+          }
+        }
+      };
+      SegStage<kDepth> A, B;
+      issue(A, 0);
+      for (uint32_t q0 = 0; q0 < Q; q0 += 2 * kDepth) {
+        issue(B, q0 + kDepth);
+        consume(A, q0);
+        issue(A, q0 + 2 * kDepth);
+        consume(B, q0 + kDepth);
       }
+      __syncthreads();  // segment list reused by the next batch; tile complete after the last
     }
-    __syncthreads();
+
+    // Write the finished tile: bytes [lt << (TL-3), ...) of this filter, up to
+    // the 16-byte-rounded bitmap length (pad bytes are zero: no position lands there).
+    const uint64_t tile_bytes = 1ull << (TL - 3);
+    const uint64_t b0 = (uint64_t)lt * tile_bytes;
+    const uint64_t nbytes = min(tile_bytes, (uint64_t)d.alloc_bytes - b0);
+    uint4 *out4 = reinterpret_cast<uint4 *>(bitmaps + d.bitmap_off + b0);
+    const uint4 *t4 = reinterpret_cast<const uint4 *>(tile);
+    for (uint32_t i = tid; i < (uint32_t)(nbytes >> 4); i += kBlockB) out4[i] = t4[i];
+    __syncthreads();  // every lane has read the tile before the next one is zeroed
   }
-
-  // Write the finished tile: bytes [lt << (TL-3), ...) of this filter, up to the
-  // 16-byte-rounded bitmap length (pad bytes are zero: no position reaches them).
-  const uint64_t tile_bytes = 1ull << (TL - 3);
-  const uint64_t b0 = (uint64_t)lt * tile_bytes;
-  const uint64_t nbytes = min(tile_bytes, (uint64_t)d.alloc_bytes - b0);
-  uint4 *out4 = reinterpret_cast<uint4 *>(bitmaps + d.bitmap_off + b0);
-  const uint4 *t4 = reinterpret_cast<const uint4 *>(tile);
-  for (uint32_t i = tid; i < (uint32_t)(nbytes >> 4); i += kBlockB) out4[i] = t4[i];
 }
 
 // ---------------------------------------------------------------- direct atomics
@@ -305,8 +425,22 @@ struct Plan {
   BuildArgs a;
   uint64_t pos_words = 0, table_words = 0, ws_bytes = 0;
   uint32_t total_chunks = 0, total_tiles = 0;
+  uint32_t grid_a = 0, grid_b = 0;  // persistent grids
   size_t lds_a = 0, lds_b = 0;
 };
+
+// Compute units of the current device (256 on MI355X), queried once.
+uint32_t device_cus() {
+  static std::once_flag once;
+  static uint32_t cus = 256;
+  std::call_once(once, [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0)
+      cus = (uint32_t)v;
+  });
+  return cus;
+}
 
 int make_plan(const uint64_t *counts, uint32_t nf, int32_t bpk, Plan &p) {
   if (nf == 0 || nf > (uint32_t)kMaxFilters || bpk < 0) return ADL_ERR_INVALID_ARG;
@@ -317,11 +451,17 @@ int make_plan(const uint64_t *counts, uint32_t nf, int32_t bpk, Plan &p) {
     if (adl_host::bitmap_bytes(counts[f], bpk) == 0) return ADL_ERR_TOO_LARGE;
     total_n += counts[f];
   }
-  uint32_t cmax = std::min<uint32_t>(kBlockA * kKptMax, kPosLdsWords / k) & ~3u;
-  uint32_t C = cmax;
-  if (total_n / cmax < kTargetWorkgroups) {
-    const uint64_t want = (total_n + kTargetWorkgroups - 1) / kTargetWorkgroups;
-    C = (uint32_t)std::min<uint64_t>(cmax, std::max<uint64_t>(256, adl_host::round_up(want, 4)));
+  // Keys per chunk: as many as the LDS holds, then evened out so the chunks
+  // split into whole rounds of the persistent grid (one workgroup per CU).
+  const uint32_t cus = device_cus();
+  const uint32_t cmax = std::min<uint32_t>(kBlockA * (k == 6 ? 6 : kKptMax), kPosLdsWords / k) & ~3u;
+  const uint64_t wmin = (total_n + cmax - 1) / cmax;
+  uint32_t C;
+  if (wmin >= cus) {
+    const uint64_t rounds = (wmin + cus - 1) / cus;
+    C = (uint32_t)std::min<uint64_t>(cmax, adl_host::round_up((total_n + rounds * cus - 1) / (rounds * cus), 4));
+  } else {
+    C = (uint32_t)std::min<uint64_t>(cmax, std::max<uint64_t>(256, adl_host::round_up((total_n + cus - 1) / cus, 4)));
   }
   uint32_t TL = kMaxTileLog2;
   auto tiles_at = [&](uint32_t tl) {
@@ -348,6 +488,8 @@ int make_plan(const uint64_t *counts, uint32_t nf, int32_t bpk, Plan &p) {
   };
   while (TL < kMaxTileLog2 && max_tiles_at(TL) + 1 > kHistMax) ++TL;
   p.a.nf = nf;
+  p.a.xcd_remap = 1;
+  if (const char *e = getenv("ADL_BLOOM_XCD_REMAP")) p.a.xcd_remap = atoi(e) != 0;
   p.a.k = k;
   p.a.C = C;
   p.a.TL = TL;
@@ -381,7 +523,9 @@ int make_plan(const uint64_t *counts, uint32_t nf, int32_t bpk, Plan &p) {
   p.table_words = adl_host::round_up(tab, 64);
   p.ws_bytes = (p.pos_words + p.table_words) * 4 + 256;
   p.lds_a = (size_t)(((kHistMax + 3) & ~3u) + 32 + k * C) * 4;
-  p.lds_b = (size_t)((1u << (TL - 5)) + (kBlockB + 4) + kBlockB + 32) * 4;
+  p.lds_b = (size_t)((1u << (TL - 5)) + 2 * kSegBatch) * 4;
+  p.grid_a = std::min<uint32_t>(p.total_chunks, cus);
+  p.grid_b = std::min<uint32_t>(p.total_tiles, cus);
   return ADL_OK;
 }
 
@@ -417,23 +561,25 @@ int launch_binned(const Plan &p, Keys keys, uint8_t *d_bitmaps, void *ws, hipStr
   if (ev) ADL_HIP_TRY(hipEventRecord(ev[0], st));
   if (p.total_chunks) {
     if (p.a.k == 6) {
-      auto kern = bloom_bin_kernel<6, Keys>;
+      auto kern = bloom_bin_kernel<6, 6, Keys>;
       ADL_HIP_TRY(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                                       (int)p.lds_a));
-      hipLaunchKernelGGL(kern, dim3(p.total_chunks), dim3(kBlockA), p.lds_a, st, p.a, keys, pos_ws, tab_ws);
+      hipLaunchKernelGGL(kern, dim3(p.grid_a), dim3(kBlockA), p.lds_a, st, p.a, keys, pos_ws, tab_ws,
+                         p.total_chunks);
     } else {
-      auto kern = bloom_bin_kernel<0, Keys>;
+      auto kern = bloom_bin_kernel<0, kKptMax, Keys>;
       ADL_HIP_TRY(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                                       (int)p.lds_a));
-      hipLaunchKernelGGL(kern, dim3(p.total_chunks), dim3(kBlockA), p.lds_a, st, p.a, keys, pos_ws, tab_ws);
+      hipLaunchKernelGGL(kern, dim3(p.grid_a), dim3(kBlockA), p.lds_a, st, p.a, keys, pos_ws, tab_ws,
+                         p.total_chunks);
     }
     ADL_HIP_TRY(hipGetLastError());
   }
   if (ev) ADL_HIP_TRY(hipEventRecord(ev[1], st));
   ADL_HIP_TRY(hipFuncSetAttribute((const void *)bloom_tile_kernel,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)p.lds_b));
-  hipLaunchKernelGGL(bloom_tile_kernel, dim3(p.total_tiles), dim3(kBlockB), p.lds_b, st, p.a,
-                     (const uint32_t *)pos_ws, (const uint32_t *)tab_ws, d_bitmaps);
+  hipLaunchKernelGGL(bloom_tile_kernel, dim3(p.grid_b), dim3(kBlockB), p.lds_b, st, p.a,
+                     (const uint32_t *)pos_ws, (const uint32_t *)tab_ws, d_bitmaps, p.total_tiles);
   ADL_HIP_TRY(hipGetLastError());
   if (ev) ADL_HIP_TRY(hipEventRecord(ev[2], st));
   return ADL_OK;
