@@ -30,6 +30,7 @@
 
 #include <algorithm>
 #include <mutex>
+#include <type_traits>
 #include <vector>
 
 #include "bloom_common.hpp"
@@ -38,21 +39,21 @@ using namespace adl_dev;
 
 namespace {
 
-constexpr int kBlockA = 1024;       // pass A threads per workgroup (16 waves)
+constexpr uint32_t kLdsWordsPerCu = 40960;  // 160 KiB of LDS per CU
 constexpr int kKptMax = 8;          // keys per thread, pass A
 constexpr int kBlockB = 1024;       // pass B threads per workgroup
-constexpr int kDepth = 8;           // segments per pipeline stage per wave, pass B (2 stages)
-constexpr int kSegBatch = 2048;     // segments staged in LDS per batch, pass B
+constexpr int kDepthB = 8;          // segments per pipeline stage per wave, pass B (ADL_BLOOM_DEPTH)
+constexpr int kSegBatch = 2048;     // segment descriptors staged in LDS per batch, pass B
+constexpr uint32_t kTablePad = 64;  // spare words after the table
 constexpr int kMaxFilters = 8;      // filters per launch pair (descriptors ride in kernargs)
 constexpr uint32_t kHistMax = 2049; // tiles per filter + 1 (m < 2^31, TL >= ... keeps T <= 2048)
-constexpr uint32_t kPosLdsWords = 36864;  // 144 KiB of sorted positions per chunk
 constexpr uint32_t kMinTileLog2 = 10;
 constexpr uint32_t kMaxTileLog2 = 20;     // 128 KiB LDS tile
 constexpr uint32_t kTargetWorkgroups = 512;
 
 struct FilterDesc {
   uint64_t key_begin;   // first key (index into the key set)
-  uint64_t pos_base;    // u32-word offset of this filter's chunk-0 region
+  uint64_t pos_base;    // word offset of this filter's chunk-0 region
   uint64_t table_base;  // u32-word offset of this filter's (tile, chunk) table
   uint64_t bitmap_off;  // output byte offset
   uint32_t n;           // keys
@@ -69,7 +70,11 @@ struct BuildArgs {
   uint32_t k;      // probes per key
   uint32_t C;      // keys per chunk
   uint32_t TL;     // log2 tile bits
-  uint32_t xcd_remap;  // pass A: consecutive chunks on one XCD (tuning, ADL_BLOOM_XCD_REMAP)
+  uint32_t cap;    // positions per chunk region (k*C; C % 4 == 0 keeps regions 16-byte aligned)
+  uint32_t hist_words;  // pass A LDS tile counters (max tiles per filter + 1, rounded to 4)
+  uint32_t xcd_remap;  // consecutive chunks / tiles on one XCD (tuning, ADL_BLOOM_XCD_REMAP)
+  uint32_t nt_keys;    // pass A: non-temporal key loads (tuning, ADL_BLOOM_NT_KEYS)
+  uint32_t nt_bitmap;  // pass B: non-temporal bitmap stores (tuning, ADL_BLOOM_NT_BITMAP)
   FilterDesc f[kMaxFilters];
 };
 
@@ -104,15 +109,15 @@ struct KeyRegs<Keys16> {
   uint4 raw;
 };
 
-// Persistent: workgroup b processes chunks b, b + gridDim.x, ...  While chunk c
-// is hashed, sorted and stored, the keys of the next chunk are already in
-// flight into registers, so the key stream overlaps the LDS work and the
-// sorted-chunk stores drain behind the next chunk's hashing.
+// Persistent, two workgroups per CU (<= 80 KiB LDS each) so one workgroup's
+// hashing overlaps the other's LDS sort and stores.  A workgroup processes
+// one chunk per round of the grid; the keys of its next chunk are already in
+// flight into registers while the current one is hashed, sorted and stored.
 //
 // KFIX > 0: k known at compile time, positions kept in registers between the
 // count and the scatter; KFIX == 0: runtime k, positions recomputed.
-template <int KFIX, int KPT, class Keys>
-__global__ __launch_bounds__(kBlockA) void bloom_bin_kernel(BuildArgs a, Keys keys,
+template <int BLOCK, int KFIX, int KPT, class Keys>
+__global__ __launch_bounds__(BLOCK) void bloom_bin_kernel(BuildArgs a, Keys keys,
                                                             uint32_t *__restrict__ pos_ws,
                                                             uint32_t *__restrict__ table_ws,
                                                             uint32_t total_chunks) {
@@ -121,10 +126,10 @@ __global__ __launch_bounds__(kBlockA) void bloom_bin_kernel(BuildArgs a, Keys ke
   const uint32_t C = a.C;
   const uint32_t k = KFIX > 0 ? (uint32_t)KFIX : a.k;
   const uint32_t TL = a.TL;
-  const uint32_t hist_words = (kHistMax + 3) & ~3u;
-  uint32_t *hist = lds;                       // T+1 counters, later cursors
-  uint32_t *scratch = lds + hist_words;       // scan scratch (BLOCK/64 + 1, padded to 32)
-  uint32_t *lpos = lds + hist_words + 32;     // k*C sorted positions
+  const uint32_t tmask = (1u << TL) - 1u;
+  uint32_t *hist = lds;                        // T+1 counters, later cursors
+  uint32_t *scratch = lds + a.hist_words;      // scan scratch (BLOCK/64 + 1, padded to 32)
+  uint32_t *lpos = lds + a.hist_words + 32;    // k*C sorted tile offsets
   constexpr bool PF = KeyRegs<Keys>::kPrefetch;
 
   auto fetch = [&](uint32_t chunk, KeyRegs<Keys> (&r)[KPT]) {
@@ -134,8 +139,11 @@ __global__ __launch_bounds__(kBlockA) void bloom_bin_kernel(BuildArgs a, Keys ke
       const uint32_t cnt = min(C, d.n - first);
 #pragma unroll
       for (int i = 0; i < KPT; ++i) {
-        const uint32_t idx = tid + i * kBlockA;
-        if (idx < cnt) r[i].raw = keys.keys[d.key_begin + first + idx];
+        const uint32_t idx = tid + i * BLOCK;
+        if (idx < cnt) {
+          const uint4 *src = keys.keys + d.key_begin + first + idx;
+          r[i].raw = a.nt_keys ? load_nt(src) : *src;
+        }
       }
     }
   };
@@ -144,15 +152,14 @@ __global__ __launch_bounds__(kBlockA) void bloom_bin_kernel(BuildArgs a, Keys ke
   // round, the 8 XCDs (blocks b, b+8, ... share one under round-robin
   // dispatch) each take G/8 consecutive chunks, so the 4-byte (tile, chunk)
   // table entries of neighbouring chunks -- one 64-byte line holds 16 -- are
-  // written from one L2 and leave it as whole lines.  Speed only: any
-  // placement gives the same result.
+  // written from one L2.  Speed only: any placement gives the same result.
   const uint32_t G = gridDim.x;
   const uint32_t slot =
       (a.xcd_remap && G % 8 == 0) ? (blockIdx.x % 8) * (G / 8) + blockIdx.x / 8 : blockIdx.x;
   const uint32_t rounds = (total_chunks + G - 1) / G;
   KeyRegs<Keys> cur[KPT];
   if (slot < total_chunks) fetch(slot, cur);
-  for (uint32_t i = tid; i < kHistMax; i += kBlockA) hist[i] = 0;
+  for (uint32_t i = tid; i < a.hist_words; i += BLOCK) hist[i] = 0;
 
   for (uint32_t r = 0; r < rounds; ++r) {
     const uint32_t wg = r * G + slot;
@@ -171,7 +178,7 @@ __global__ __launch_bounds__(kBlockA) void bloom_bin_kernel(BuildArgs a, Keys ke
     uint32_t h1[KPT], h2[KPT];
 #pragma unroll
     for (int i = 0; i < KPT; ++i) {
-      const uint32_t idx = tid + i * kBlockA;
+      const uint32_t idx = tid + i * BLOCK;
       h1[i] = h2[i] = 0;
       if (idx < cnt) {
         if constexpr (PF) hash16(cur[i].raw, h1[i], h2[i]);
@@ -184,7 +191,7 @@ __global__ __launch_bounds__(kBlockA) void bloom_bin_kernel(BuildArgs a, Keys ke
     uint32_t pos[KPT][KR];
 #pragma unroll
     for (int i = 0; i < KPT; ++i) {
-      const uint32_t idx = tid + i * kBlockA;
+      const uint32_t idx = tid + i * BLOCK;
       if (idx < cnt) {
         if constexpr (KFIX > 0) {
 #pragma unroll
@@ -203,46 +210,46 @@ __global__ __launch_bounds__(kBlockA) void bloom_bin_kernel(BuildArgs a, Keys ke
     __syncthreads();
 
     // Exclusive scan: hist[t] = start of tile t's run; hist[T] = k*cnt.
-    block_excl_scan_array<kBlockA>(hist, T + 1, scratch);
+    block_excl_scan_array<BLOCK>(hist, T + 1, scratch);
 
     // (tile, chunk) table, T+1 rows of W entries: row t = start of tile t.
     uint32_t *tab = table_ws + d.table_base;
-    for (uint32_t t = tid; t <= T; t += kBlockA) tab[(uint64_t)t * d.chunks + w] = hist[t];
+    for (uint32_t t = tid; t <= T; t += BLOCK) tab[(uint64_t)t * d.chunks + w] = hist[t];
     __syncthreads();
 
-    // Scatter into LDS by tile (hist now serves as the per-tile cursor).
+    // Scatter tile offsets into LDS by tile (hist now serves as the cursor).
 #pragma unroll
     for (int i = 0; i < KPT; ++i) {
-      const uint32_t idx = tid + i * kBlockA;
+      const uint32_t idx = tid + i * BLOCK;
       if (idx < cnt) {
         if constexpr (KFIX > 0) {
+          // all k cursor bumps in flight before the first dependent write
+          uint32_t slot_l[KFIX];
 #pragma unroll
-          for (int j = 0; j < KFIX; ++j) {
-            const uint32_t slot = atomicAdd(&hist[pos[i][j] >> TL], 1u);
-            lpos[slot] = pos[i][j];
-          }
+          for (int j = 0; j < KFIX; ++j) slot_l[j] = atomicAdd(&hist[pos[i][j] >> TL], 1u);
+#pragma unroll
+          for (int j = 0; j < KFIX; ++j) lpos[slot_l[j]] = pos[i][j] & tmask;
         } else {
           for (uint32_t j = 0; j < k; ++j) {
             const uint32_t p = fastmod(h1[i] + j * h2[i], mod);
-            const uint32_t slot = atomicAdd(&hist[p >> TL], 1u);
-            lpos[slot] = p;
+            const uint32_t slot_l = atomicAdd(&hist[p >> TL], 1u);
+            lpos[slot_l] = p & tmask;
           }
         }
       }
     }
     __syncthreads();
 
-    // Stream the sorted chunk out: k*cnt words, region w is k*C words long
-    // (16-byte aligned because C % 4 == 0 and pos_base % 4 == 0).  The hist
-    // is cleared for the next chunk meanwhile (the scatter is done with it).
-    for (uint32_t i = tid; i <= T; i += kBlockA) hist[i] = 0;
+    // Stream the sorted chunk out to region w (a.cap positions, 16-byte
+    // aligned).  The hist is cleared for the next chunk meanwhile.
+    for (uint32_t i = tid; i <= T; i += BLOCK) hist[i] = 0;
     const uint32_t total = k * cnt;
-    uint32_t *dst = pos_ws + d.pos_base + (uint64_t)w * k * C;
+    uint32_t *dst = pos_ws + d.pos_base + (uint64_t)w * a.cap;
     const uint32_t nvec = total >> 2;
     const uint4 *src4 = reinterpret_cast<const uint4 *>(lpos);
     uint4 *dst4 = reinterpret_cast<uint4 *>(dst);
-    for (uint32_t i = tid; i < nvec; i += kBlockA) dst4[i] = src4[i];
-    for (uint32_t i = (nvec << 2) + tid; i < total; i += kBlockA) dst[i] = lpos[i];
+    for (uint32_t i = tid; i < nvec; i += BLOCK) dst4[i] = src4[i];
+    for (uint32_t i = (nvec << 2) + tid; i < total; i += BLOCK) dst[i] = lpos[i];
 
     if constexpr (PF) {
 #pragma unroll
@@ -252,19 +259,19 @@ __global__ __launch_bounds__(kBlockA) void bloom_bin_kernel(BuildArgs a, Keys ke
 }
 
 // ---------------------------------------------------------------- pass B
-// Persistent: workgroup b owns tiles b, b + gridDim.x, ...  For a tile, the
-// (tile, chunk) table rows give one segment per chunk region.  A wave takes
-// whole segments (segment j -> wave j % 16) and reads up to 2 x 64 positions
-// of each with two predicated wave-loads (no per-element search), through a
-// two-stage register pipeline: the loads of the next kDepth segments are in
-// flight while the current kDepth are ds_or_b32'd into the LDS tile.  The next
-// tile's table rows are prefetched into registers during the gather, and the
-// finished tile's 16-byte stores drain while the next tile starts.
-template <int DEPTH>
-struct SegStage {
-  uint32_t v0[DEPTH], v1[DEPTH];
-};
-
+// Persistent: workgroup b owns the tiles of slot(b) in every round.  For a
+// tile, the (tile, chunk) table rows give one segment per chunk region.  The
+// segment list {start, length} is staged in LDS (its rows for the next tile
+// are prefetched into registers during the current tile's gather).  A wave
+// takes segments j = wave + 16q and runs a two-stage register pipeline over
+// them: a stage's D descriptors are read with one ds_read_b64 per lane and
+// handed to the slots by readlane (no load waits on LDS); every slot gathers
+// positions 0..63 of its segment with one wave-load and 64..127 with a second
+// when the segment is that long, so the loads of the next stage are in flight
+// while the current stage is ds_or_b32'd into the LDS tile.  The rare longer
+// segments (hot tiles) finish in a 4-deep unrolled loop.  The finished tile's
+// 16-byte stores drain while the next tile is zeroed.
+template <int D>
 __global__ __launch_bounds__(kBlockB) void bloom_tile_kernel(BuildArgs a,
                                                              const uint32_t *__restrict__ pos_ws,
                                                              const uint32_t *__restrict__ table_ws,
@@ -276,11 +283,8 @@ __global__ __launch_bounds__(kBlockB) void bloom_tile_kernel(BuildArgs a,
   constexpr int RPT = kSegBatch / kBlockB;  // table entries per thread per batch
   const uint32_t TL = a.TL;
   const uint32_t tile_words = 1u << (TL - 5);
-  const uint32_t tmask = (1u << TL) - 1u;
-  const uint32_t region = a.k * a.C;
-  uint32_t *tile = lds;                    // 2^TL bits
-  uint32_t *sbase = lds + tile_words;      // kSegBatch segment start words
-  uint32_t *slen = sbase + kSegBatch;      // kSegBatch segment lengths
+  uint32_t *tile = lds;                                      // 2^TL bits
+  uint2 *seg = reinterpret_cast<uint2 *>(lds + tile_words);  // kSegBatch {start word, length}
 
   auto fetch_rows = [&](uint32_t wg, uint32_t wb, uint32_t (&rs)[RPT], uint32_t (&re)[RPT]) {
     const FilterDesc &d = a.f[find_filter_by_tile(a, wg)];
@@ -290,24 +294,26 @@ __global__ __launch_bounds__(kBlockB) void bloom_tile_kernel(BuildArgs a,
     for (int r = 0; r < RPT; ++r) {
       const uint32_t i = wb + tid + r * kBlockB;
       rs[r] = re[r] = 0;
-      if (i < W && (uint32_t)(tid + r * kBlockB) < (uint32_t)kSegBatch) {
+      if (i < W) {
         rs[r] = row0[i];
         re[r] = row0[i + W];
       }
     }
   };
+  auto or_pos = [&](uint32_t off) { atomicOr(&tile[off >> 5], 1u << (off & 31)); };
 
-  auto or_pos = [&](uint32_t v) {
-    const uint32_t off = v & tmask;
-    atomicOr(&tile[off >> 5], 1u << (off & 31));
-  };
-
+  // Round r covers tiles [r*G, (r+1)*G); inside a round each XCD takes G/8
+  // consecutive tiles, so the line a tile's segment shares with its
+  // neighbour's (segments of consecutive tiles are adjacent in every chunk
+  // region) is fetched into one L2 once.  Speed only.
+  const uint32_t G = gridDim.x;
+  const uint32_t slot =
+      (a.xcd_remap && G % 8 == 0) ? (blockIdx.x % 8) * (G / 8) + blockIdx.x / 8 : blockIdx.x;
   uint32_t pre_s[RPT], pre_e[RPT];
-  if (blockIdx.x < total_tiles) fetch_rows(blockIdx.x, 0, pre_s, pre_e);
+  if (slot < total_tiles) fetch_rows(slot, 0, pre_s, pre_e);
 
-  for (uint32_t wg = blockIdx.x; wg < total_tiles; wg += gridDim.x) {
-    const int fi = find_filter_by_tile(a, wg);
-    const FilterDesc &d = a.f[fi];
+  for (uint32_t wg = slot; wg < total_tiles; wg += G) {
+    const FilterDesc &d = a.f[find_filter_by_tile(a, wg)];
     const uint32_t lt = wg - d.tile_base;
     const uint32_t W = d.chunks;
     const uint32_t pos_base = (uint32_t)d.pos_base;
@@ -315,7 +321,7 @@ __global__ __launch_bounds__(kBlockB) void bloom_tile_kernel(BuildArgs a,
     uint4 *t4w = reinterpret_cast<uint4 *>(tile);
     for (uint32_t i = tid; i < tile_words / 4; i += kBlockB) t4w[i] = make_uint4(0, 0, 0, 0);
     // an empty filter (no chunks) has no batch to prefetch the next tile from
-    if (W == 0 && wg + gridDim.x < total_tiles) fetch_rows(wg + gridDim.x, 0, pre_s, pre_e);
+    if (W == 0 && wg + G < total_tiles) fetch_rows(wg + G, 0, pre_s, pre_e);
     __syncthreads();  // tile zeroed (also when W == 0)
 
     for (uint32_t wb = 0; wb < W; wb += kSegBatch) {
@@ -330,52 +336,61 @@ __global__ __launch_bounds__(kBlockB) void bloom_tile_kernel(BuildArgs a,
 #pragma unroll
       for (int r = 0; r < RPT; ++r) {
         const uint32_t i = tid + r * kBlockB;
-        if (i < nw) {
-          sbase[i] = pos_base + (wb + i) * region + rs[r];
-          slen[i] = re[r] - rs[r];
-        }
+        if (i < nw) seg[i] = make_uint2(pos_base + (wb + i) * a.cap + rs[r], re[r] - rs[r]);
       }
-      __syncthreads();  // segment list ready (and the tile zeroed)
-      if (wb + kSegBatch >= W && wg + gridDim.x < total_tiles) fetch_rows(wg + gridDim.x, 0, pre_s, pre_e);
+      __syncthreads();  // segment list ready
+      if (wb + kSegBatch >= W && wg + G < total_tiles) fetch_rows(wg + G, 0, pre_s, pre_e);
 
-      // this wave's segments: j = wave + NWAVES * q, q < Q
       const uint32_t Q = nw > (uint32_t)wave ? (nw - wave + NWAVES - 1) / NWAVES : 0;
-      auto issue = [&](SegStage<kDepth> &st, uint32_t q0) {
+      struct Stage {
+        uint32_t v0[D], v1[D];
+        uint32_t base, len;  // lane u: descriptor of slot u
+      };
+      auto issue = [&](Stage &st, uint32_t q0) {
+        const uint32_t q = q0 + lane;
+        uint2 dsc = make_uint2(0, 0);
+        if (lane < D && q < Q) dsc = seg[wave + NWAVES * q];
+        st.base = dsc.x;
+        st.len = dsc.y;
 #pragma unroll
-        for (int u = 0; u < kDepth; ++u) {
-          const uint32_t q = q0 + u;
-          st.v0[u] = st.v1[u] = 0;
-          if (q < Q) {
-            const uint32_t j = wave + NWAVES * q;
-            const uint32_t len = slen[j], b = sbase[j];
-            if ((uint32_t)lane < len) st.v0[u] = pos_ws[b + lane];
-            if ((uint32_t)lane + kWave < len) st.v1[u] = pos_ws[b + kWave + lane];
-          }
+        for (int u = 0; u < D; ++u) {
+          const uint32_t len = __builtin_amdgcn_readlane(st.len, u);
+          const uint32_t b = __builtin_amdgcn_readlane(st.base, u);
+          if ((uint32_t)lane < len) st.v0[u] = pos_ws[b + lane];
+          if (len > (uint32_t)kWave && (uint32_t)lane + kWave < len) st.v1[u] = pos_ws[b + kWave + lane];
         }
       };
-      auto consume = [&](const SegStage<kDepth> &st, uint32_t q0) {
+      auto consume = [&](const Stage &st) {
 #pragma unroll
-        for (int u = 0; u < kDepth; ++u) {
-          const uint32_t q = q0 + u;
-          if (q < Q) {
-            const uint32_t j = wave + NWAVES * q;
-            const uint32_t len = slen[j];
-            if ((uint32_t)lane < len) or_pos(st.v0[u]);
+        for (int u = 0; u < D; ++u) {
+          const uint32_t len = __builtin_amdgcn_readlane(st.len, u);
+          if ((uint32_t)lane < len) or_pos(st.v0[u]);
+          if (len > (uint32_t)kWave) {
             if ((uint32_t)lane + kWave < len) or_pos(st.v1[u]);
-            if (len > 2u * kWave) {  // rare: long segments of hot tiles
-              const uint32_t b = sbase[j];
-              for (uint32_t o = 2 * kWave + lane; o < len; o += kWave) or_pos(pos_ws[b + o]);
+            if (len > 2u * kWave) {  // long segments (hot tiles): 4 loads in flight
+              const uint32_t b = __builtin_amdgcn_readlane(st.base, u);
+              for (uint32_t o = 2 * kWave; o < len; o += 4 * kWave) {
+                uint32_t x[4];
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                  const uint32_t e = o + t * kWave + lane;
+                  x[t] = e < len ? pos_ws[b + e] : 0u;
+                }
+#pragma unroll
+                for (int t = 0; t < 4; ++t)
+                  if (o + t * kWave + lane < len) or_pos(x[t]);
+              }
             }
           }
         }
       };
-      SegStage<kDepth> A, B;
+      Stage A, B;
       issue(A, 0);
-      for (uint32_t q0 = 0; q0 < Q; q0 += 2 * kDepth) {
-        issue(B, q0 + kDepth);
-        consume(A, q0);
-        issue(A, q0 + 2 * kDepth);
-        consume(B, q0 + kDepth);
+      for (uint32_t q0 = 0; q0 < Q; q0 += 2 * D) {
+        issue(B, q0 + D);
+        consume(A);
+        issue(A, q0 + 2 * D);
+        consume(B);
       }
       __syncthreads();  // segment list reused by the next batch; tile complete after the last
     }
@@ -387,7 +402,11 @@ __global__ __launch_bounds__(kBlockB) void bloom_tile_kernel(BuildArgs a,
     const uint64_t nbytes = min(tile_bytes, (uint64_t)d.alloc_bytes - b0);
     uint4 *out4 = reinterpret_cast<uint4 *>(bitmaps + d.bitmap_off + b0);
     const uint4 *t4 = reinterpret_cast<const uint4 *>(tile);
-    for (uint32_t i = tid; i < (uint32_t)(nbytes >> 4); i += kBlockB) out4[i] = t4[i];
+    if (a.nt_bitmap) {
+      for (uint32_t i = tid; i < (uint32_t)(nbytes >> 4); i += kBlockB) store_nt(out4 + i, t4[i]);
+    } else {
+      for (uint32_t i = tid; i < (uint32_t)(nbytes >> 4); i += kBlockB) out4[i] = t4[i];
+    }
     __syncthreads();  // every lane has read the tile before the next one is zeroed
   }
 }
@@ -426,8 +445,20 @@ struct Plan {
   uint64_t pos_words = 0, table_words = 0, ws_bytes = 0;
   uint32_t total_chunks = 0, total_tiles = 0;
   uint32_t grid_a = 0, grid_b = 0;  // persistent grids
+  uint32_t block_a = 512;             // pass A threads per workgroup
+  uint32_t depth = kDepthB;           // pass B descriptors per step
   size_t lds_a = 0, lds_b = 0;
 };
+
+uint32_t env_flag(const char *name, uint32_t dflt) {
+  const char *e = getenv(name);
+  return e ? (uint32_t)(atoi(e) != 0) : dflt;
+}
+
+uint32_t env_u32(const char *name, uint32_t dflt) {
+  const char *e = getenv(name);
+  return e ? (uint32_t)atoi(e) : dflt;
+}
 
 // Compute units of the current device (256 on MI355X), queried once.
 uint32_t device_cus() {
@@ -451,48 +482,61 @@ int make_plan(const uint64_t *counts, uint32_t nf, int32_t bpk, Plan &p) {
     if (adl_host::bitmap_bytes(counts[f], bpk) == 0) return ADL_ERR_TOO_LARGE;
     total_n += counts[f];
   }
-  // Keys per chunk: as many as the LDS holds, then evened out so the chunks
-  // split into whole rounds of the persistent grid (one workgroup per CU).
-  const uint32_t cus = device_cus();
-  const uint32_t cmax = std::min<uint32_t>(kBlockA * (k == 6 ? 6 : kKptMax), kPosLdsWords / k) & ~3u;
-  const uint64_t wmin = (total_n + cmax - 1) / cmax;
-  uint32_t C;
-  if (wmin >= cus) {
-    const uint64_t rounds = (wmin + cus - 1) / cus;
-    C = (uint32_t)std::min<uint64_t>(cmax, adl_host::round_up((total_n + rounds * cus - 1) / (rounds * cus), 4));
-  } else {
-    C = (uint32_t)std::min<uint64_t>(cmax, std::max<uint64_t>(256, adl_host::round_up((total_n + cus - 1) / cus, 4)));
-  }
+  // Tile size: the largest (fewest, longest segments) that still yields
+  // enough pass-B workgroups; every filter's tile histogram must fit the
+  // pass-A counters (T + 1 <= kHistMax).
   uint32_t TL = kMaxTileLog2;
-  auto tiles_at = [&](uint32_t tl) {
+  auto tiles_at = [&](uint32_t tl, bool max_only) {
     uint64_t t = 0;
     for (uint32_t f = 0; f < nf; ++f) {
       const uint64_t m = adl_host::bitmap_bytes(counts[f], bpk) * 8;
-      t += (m + (1ull << tl) - 1) >> tl;
+      const uint64_t tf = (m + (1ull << tl) - 1) >> tl;
+      t = max_only ? std::max<uint64_t>(t, tf) : t + tf;
     }
     return t;
   };
-  while (TL > kMinTileLog2 && tiles_at(TL) < kTargetWorkgroups) --TL;
+  while (TL > kMinTileLog2 && tiles_at(TL, false) < kTargetWorkgroups) --TL;
   if (const char *e = getenv("ADL_BLOOM_TILE_LOG2")) {  // tuning override
     const int v = atoi(e);
     if (v >= (int)kMinTileLog2 && v <= (int)kMaxTileLog2) TL = (uint32_t)v;
   }
-  // every filter's tile histogram must fit the LDS counters (T + 1 <= kHistMax)
-  auto max_tiles_at = [&](uint32_t tl) {
-    uint64_t t = 0;
-    for (uint32_t f = 0; f < nf; ++f) {
-      const uint64_t m = adl_host::bitmap_bytes(counts[f], bpk) * 8;
-      t = std::max<uint64_t>(t, (m + (1ull << tl) - 1) >> tl);
-    }
-    return t;
-  };
-  while (TL < kMaxTileLog2 && max_tiles_at(TL) + 1 > kHistMax) ++TL;
+  while (TL < kMaxTileLog2 && tiles_at(TL, true) + 1 > kHistMax) ++TL;
+  const uint32_t hist_words = (uint32_t)adl_host::round_up(tiles_at(TL, true) + 1, 4);
+
+  // Keys per chunk: as many as the rest of the pass-A LDS holds, then evened
+  // out so the chunks split into whole rounds of the persistent grid.
+  // Pass A geometry (ADL_BLOOM_A_WGS_PER_CU): 2 x 512 threads per CU overlap
+  // one workgroup's hashing with the other's LDS sort; 1 x 1024 threads per
+  // CU doubles the chunk, so pass B gathers half as many, twice as long
+  // segments.
+  const uint32_t cus = device_cus();
+  const uint32_t bpc = env_u32("ADL_BLOOM_A_WGS_PER_CU", 1) == 2 ? 2 : 1;
+  const uint32_t block_a = bpc == 1 ? 1024 : 512;
+  const uint32_t grid_a_max = bpc * cus;
+  const uint32_t kpt = k == 6 ? 6 : kKptMax;
+  const uint32_t lds_words_a = kLdsWordsPerCu / bpc - (bpc == 1 ? 256 : 0);
+  const uint32_t cmax = std::min<uint32_t>(block_a * kpt, (lds_words_a - hist_words - 32) / k) & ~3u;
+  if (cmax < 4) return ADL_ERR_TOO_LARGE;
+  const uint64_t wmin = (total_n + cmax - 1) / cmax;
+  uint32_t C;
+  if (wmin >= grid_a_max) {
+    const uint64_t rounds = (wmin + grid_a_max - 1) / grid_a_max;
+    C = (uint32_t)std::min<uint64_t>(
+        cmax, adl_host::round_up((total_n + rounds * grid_a_max - 1) / (rounds * grid_a_max), 4));
+  } else {
+    C = (uint32_t)std::min<uint64_t>(
+        cmax, std::max<uint64_t>(256, adl_host::round_up((total_n + grid_a_max - 1) / grid_a_max, 4)));
+  }
   p.a.nf = nf;
-  p.a.xcd_remap = 1;
-  if (const char *e = getenv("ADL_BLOOM_XCD_REMAP")) p.a.xcd_remap = atoi(e) != 0;
+  p.a.xcd_remap = env_flag("ADL_BLOOM_XCD_REMAP", 1);
+  p.a.nt_keys = env_flag("ADL_BLOOM_NT_KEYS", 1);
+  p.a.nt_bitmap = env_flag("ADL_BLOOM_NT_BITMAP", 1);
   p.a.k = k;
   p.a.C = C;
   p.a.TL = TL;
+  const uint32_t cap = k * C;
+  p.a.cap = cap;
+  p.a.hist_words = hist_words;
   uint64_t pos = 0, tab = 0, boff = 0;
   uint32_t chunk = 0, tile = 0;
   for (uint32_t f = 0; f < nf; ++f) {
@@ -513,18 +557,20 @@ int make_plan(const uint64_t *counts, uint32_t nf, int32_t bpk, Plan &p) {
     d.key_begin = 0;      // overwritten by the caller
     chunk += d.chunks;
     tile += d.tiles;
-    pos += (uint64_t)d.chunks * k * C;
+    pos += (uint64_t)d.chunks * cap;
     tab += (uint64_t)(d.tiles + 1) * d.chunks;
   }
-  if (pos >= (1ull << 32)) return ADL_ERR_TOO_LARGE;  // pass B addresses in u32 words
+  if (pos + 64 >= (1ull << 32)) return ADL_ERR_TOO_LARGE;  // u32 position indices
   p.total_chunks = chunk;
   p.total_tiles = tile;
   p.pos_words = adl_host::round_up(pos, 64);
-  p.table_words = adl_host::round_up(tab, 64);
+  p.table_words = adl_host::round_up(tab + kTablePad, 64);
   p.ws_bytes = (p.pos_words + p.table_words) * 4 + 256;
-  p.lds_a = (size_t)(((kHistMax + 3) & ~3u) + 32 + k * C) * 4;
+  p.lds_a = (size_t)(hist_words + 32 + k * C) * 4;
   p.lds_b = (size_t)((1u << (TL - 5)) + 2 * kSegBatch) * 4;
-  p.grid_a = std::min<uint32_t>(p.total_chunks, cus);
+  p.grid_a = std::min<uint32_t>(p.total_chunks, grid_a_max);
+  p.block_a = block_a;
+  p.depth = env_u32("ADL_BLOOM_DEPTH", kDepthB);
   p.grid_b = std::min<uint32_t>(p.total_tiles, cus);
   return ADL_OK;
 }
@@ -560,27 +606,36 @@ int launch_binned(const Plan &p, Keys keys, uint8_t *d_bitmaps, void *ws, hipStr
   hipEvent_t *ev = prof_slot();
   if (ev) ADL_HIP_TRY(hipEventRecord(ev[0], st));
   if (p.total_chunks) {
-    if (p.a.k == 6) {
-      auto kern = bloom_bin_kernel<6, 6, Keys>;
+    auto go = [&](auto kern) -> int {
       ADL_HIP_TRY(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                                       (int)p.lds_a));
-      hipLaunchKernelGGL(kern, dim3(p.grid_a), dim3(kBlockA), p.lds_a, st, p.a, keys, pos_ws, tab_ws,
+      hipLaunchKernelGGL(kern, dim3(p.grid_a), dim3(p.block_a), p.lds_a, st, p.a, keys, pos_ws, tab_ws,
                          p.total_chunks);
-    } else {
-      auto kern = bloom_bin_kernel<0, kKptMax, Keys>;
-      ADL_HIP_TRY(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      (int)p.lds_a));
-      hipLaunchKernelGGL(kern, dim3(p.grid_a), dim3(kBlockA), p.lds_a, st, p.a, keys, pos_ws, tab_ws,
-                         p.total_chunks);
-    }
-    ADL_HIP_TRY(hipGetLastError());
+      ADL_HIP_TRY(hipGetLastError());
+      return ADL_OK;
+    };
+    auto by_block = [&](auto k6, auto kgen) -> int {  // k6/kgen: tag types carrying BLOCK
+      constexpr int B = decltype(k6)::value;
+      if (p.a.k == 6) return go(bloom_bin_kernel<B, 6, 6, Keys>);
+      return go(bloom_bin_kernel<B, 0, kKptMax, Keys>);
+    };
+    const int rc = p.block_a == 1024 ? by_block(std::integral_constant<int, 1024>{}, 0)
+                                     : by_block(std::integral_constant<int, 512>{}, 0);
+    if (rc) return rc;
   }
   if (ev) ADL_HIP_TRY(hipEventRecord(ev[1], st));
-  ADL_HIP_TRY(hipFuncSetAttribute((const void *)bloom_tile_kernel,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)p.lds_b));
-  hipLaunchKernelGGL(bloom_tile_kernel, dim3(p.grid_b), dim3(kBlockB), p.lds_b, st, p.a,
-                     (const uint32_t *)pos_ws, (const uint32_t *)tab_ws, d_bitmaps, p.total_tiles);
-  ADL_HIP_TRY(hipGetLastError());
+  auto go_b = [&](auto kern) -> int {
+    ADL_HIP_TRY(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)p.lds_b));
+    hipLaunchKernelGGL(kern, dim3(p.grid_b), dim3(kBlockB), p.lds_b, st, p.a, (const uint32_t *)pos_ws,
+                       (const uint32_t *)tab_ws, d_bitmaps, p.total_tiles);
+    ADL_HIP_TRY(hipGetLastError());
+    return ADL_OK;
+  };
+  int rcb;
+  if (p.depth <= 8) rcb = go_b(bloom_tile_kernel<8>);
+  else if (p.depth <= 12) rcb = go_b(bloom_tile_kernel<12>);
+  else rcb = go_b(bloom_tile_kernel<16>);
+  if (rcb) return rcb;
   if (ev) ADL_HIP_TRY(hipEventRecord(ev[2], st));
   return ADL_OK;
 }

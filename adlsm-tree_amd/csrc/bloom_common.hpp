@@ -48,6 +48,21 @@ struct KeysVar {
   }
 };
 
+// ---------------------------------------------------------------- nt access
+// Non-temporal 16-byte load/store (global_*_dwordx4 ... nt): streamed data that
+// should not displace what the next kernel re-reads from L2 / Infinity Cache.
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint4 load_nt(const uint4 *p) {
+  const u32x4_t v = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t *>(p));
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+__device__ __forceinline__ void store_nt(uint4 *p, uint4 v) {
+  const u32x4_t x = {v.x, v.y, v.z, v.w};
+  __builtin_nontemporal_store(x, reinterpret_cast<u32x4_t *>(p));
+}
+
 // ---------------------------------------------------------------- scans
 // Inclusive wave64 scan.
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {
