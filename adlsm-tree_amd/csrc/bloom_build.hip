@@ -258,6 +258,132 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin_kernel(BuildArgs a, Keys keys
   }
 }
 
+// Pass A for the hot path (16-byte keys, compile-time k).  Same output as
+// bloom_bin_kernel, with the chunk loop software-pipelined so VALU, LDS and
+// memory overlap inside one workgroup:
+//   count(c)   [fastmod + ds_add]          interleaved with  store(c-1)  [ds_read_b128 + global stores]
+//   scan(c), table(c)
+//   scatter(c) [ds_add_rtn + ds_write]     interleaved with  hash(c+1)   [murmur VALU]
+//   prefetch keys of c+2
+// so the murmur work hides under the scatter's LDS latency and the position
+// stores drain under the next count.
+template <int BLOCK, int K>
+__global__ __launch_bounds__(BLOCK) void bloom_bin16_kernel(BuildArgs a, Keys16 keys,
+                                                              uint32_t *__restrict__ pos_ws,
+                                                              uint32_t *__restrict__ table_ws,
+                                                              uint32_t total_chunks) {
+  constexpr int KPT = 6;                    // keys per thread (C <= 6 * BLOCK)
+  constexpr int VPT = (K * KPT + 3) / 4;    // 16-byte stores per thread per chunk, at most
+  constexpr int SPI = (VPT + KPT - 1) / KPT;  // of those, per count iteration
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  const int tid = threadIdx.x;
+  const uint32_t C = a.C;
+  const uint32_t TL = a.TL;
+  const uint32_t tmask = (1u << TL) - 1u;
+  uint32_t *hist = lds;                        // T+1 counters, later cursors
+  uint32_t *scratch = lds + a.hist_words;      // scan scratch
+  uint32_t *lpos = lds + a.hist_words + 32;    // K*C sorted tile offsets
+  const uint4 *src4 = reinterpret_cast<const uint4 *>(lpos);
+
+  const uint32_t G = gridDim.x;
+  const uint32_t slot =
+      (a.xcd_remap && G % 8 == 0) ? (blockIdx.x % 8) * (G / 8) + blockIdx.x / 8 : blockIdx.x;
+
+  auto chunk_cnt = [&](uint32_t chunk) -> uint32_t {
+    const FilterDesc &d = a.f[find_filter_by_chunk(a, chunk)];
+    return min(C, d.n - (chunk - d.chunk_base) * C);
+  };
+  auto fetch = [&](uint32_t chunk, uint4 (&raw)[KPT]) {
+    const FilterDesc &d = a.f[find_filter_by_chunk(a, chunk)];
+    const uint32_t first = (chunk - d.chunk_base) * C;
+    const uint32_t cnt = min(C, d.n - first);
+#pragma unroll
+    for (int i = 0; i < KPT; ++i) {
+      const uint32_t idx = tid + i * BLOCK;
+      if (idx < cnt) {
+        const uint4 *src = keys.keys + d.key_begin + first + idx;
+        raw[i] = a.nt_keys ? load_nt(src) : *src;
+      }
+    }
+  };
+
+  uint4 raw[KPT];
+  uint32_t h1[KPT], h2[KPT];
+  if (slot >= total_chunks) return;
+  {
+    fetch(slot, raw);
+    const uint32_t cnt0 = chunk_cnt(slot);
+#pragma unroll
+    for (int i = 0; i < KPT; ++i)
+      if (tid + i * BLOCK < cnt0) hash16(raw[i], h1[i], h2[i]);
+    if (slot + G < total_chunks) fetch(slot + G, raw);
+  }
+  for (uint32_t i = tid; i < a.hist_words; i += BLOCK) hist[i] = 0;
+
+  uint4 *pdst = nullptr;  // deferred store of the previous chunk
+  uint32_t ptotal = 0;
+  for (uint32_t wg = slot; wg < total_chunks; wg += G) {
+    const FilterDesc &d = a.f[find_filter_by_chunk(a, wg)];
+    const uint32_t w = wg - d.chunk_base;
+    const uint32_t cnt = min(C, d.n - w * C);
+    const uint32_t T = d.tiles;
+    const FastMod mod = d.mod;
+    __syncthreads();  // hist cleared; the previous scatter is complete in lpos
+
+    // count(c) + store(c-1)
+    const uint32_t pvec = ptotal >> 2;
+    uint32_t pos[KPT][K];
+#pragma unroll
+    for (int i = 0; i < KPT; ++i) {
+      if (tid + i * BLOCK < cnt) {
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+          pos[i][j] = fastmod(h1[i] + (uint32_t)j * h2[i], mod);
+          atomicAdd(&hist[pos[i][j] >> TL], 1u);
+        }
+      }
+#pragma unroll
+      for (int sv = i * SPI; sv < (i + 1) * SPI && sv < VPT; ++sv) {
+        const uint32_t v = tid + sv * BLOCK;
+        if (v < pvec) pdst[v] = src4[v];
+      }
+    }
+    if ((uint32_t)tid < (ptotal & 3u))
+      reinterpret_cast<uint32_t *>(pdst)[pvec * 4 + tid] = lpos[pvec * 4 + tid];
+    __syncthreads();  // counts complete; the previous chunk's LDS copy is read out
+
+    block_excl_scan_array<BLOCK>(hist, T + 1, scratch);
+    uint32_t *tab = table_ws + d.table_base;
+    for (uint32_t t = tid; t <= T; t += BLOCK) tab[(uint64_t)t * d.chunks + w] = hist[t];
+    __syncthreads();
+
+    // scatter(c) + hash(c+1) (its keys arrived during the previous chunk)
+    const bool has_next = wg + G < total_chunks;
+    const uint32_t cnt_n = has_next ? chunk_cnt(wg + G) : 0u;
+#pragma unroll
+    for (int i = 0; i < KPT; ++i) {
+      if (tid + i * BLOCK < cnt) {
+        uint32_t sl[K];
+#pragma unroll
+        for (int j = 0; j < K; ++j) sl[j] = atomicAdd(&hist[pos[i][j] >> TL], 1u);
+#pragma unroll
+        for (int j = 0; j < K; ++j) lpos[sl[j]] = pos[i][j] & tmask;
+      }
+      if (tid + i * BLOCK < cnt_n) hash16(raw[i], h1[i], h2[i]);
+    }
+    if (wg + 2 * G < total_chunks) fetch(wg + 2 * G, raw);
+    __syncthreads();  // lpos holds chunk c sorted; hist is free
+    for (uint32_t i = tid; i <= T; i += BLOCK) hist[i] = 0;
+    pdst = reinterpret_cast<uint4 *>(pos_ws + d.pos_base + (uint64_t)w * a.cap);
+    ptotal = K * cnt;
+  }
+  // epilogue: the last chunk's store
+  const uint32_t pvec = ptotal >> 2;
+  for (uint32_t v = tid; v < pvec; v += BLOCK) pdst[v] = src4[v];
+  if ((uint32_t)tid < (ptotal & 3u))
+    reinterpret_cast<uint32_t *>(pdst)[pvec * 4 + tid] = lpos[pvec * 4 + tid];
+}
+
 // ---------------------------------------------------------------- pass B
 // Persistent: workgroup b owns the tiles of slot(b) in every round.  For a
 // tile, the (tile, chunk) table rows give one segment per chunk region.  The
@@ -447,6 +573,7 @@ struct Plan {
   uint32_t grid_a = 0, grid_b = 0;  // persistent grids
   uint32_t block_a = 512;             // pass A threads per workgroup
   uint32_t depth = kDepthB;           // pass B descriptors per step
+  bool sequential_a = false;          // ADL_BLOOM_SEQ_A=1: the unpipelined pass A (A/B tuning)
   size_t lds_a = 0, lds_b = 0;
 };
 
@@ -571,6 +698,7 @@ int make_plan(const uint64_t *counts, uint32_t nf, int32_t bpk, Plan &p) {
   p.grid_a = std::min<uint32_t>(p.total_chunks, grid_a_max);
   p.block_a = block_a;
   p.depth = env_u32("ADL_BLOOM_DEPTH", kDepthB);
+  p.sequential_a = env_flag("ADL_BLOOM_SEQ_A", 0) != 0;
   p.grid_b = std::min<uint32_t>(p.total_tiles, cus);
   return ADL_OK;
 }
@@ -616,6 +744,9 @@ int launch_binned(const Plan &p, Keys keys, uint8_t *d_bitmaps, void *ws, hipStr
     };
     auto by_block = [&](auto k6, auto kgen) -> int {  // k6/kgen: tag types carrying BLOCK
       constexpr int B = decltype(k6)::value;
+      if constexpr (std::is_same<Keys, Keys16>::value) {
+        if (p.a.k == 6 && !p.sequential_a) return go(bloom_bin16_kernel<B, 6>);
+      }
       if (p.a.k == 6) return go(bloom_bin_kernel<B, 6, 6, Keys>);
       return go(bloom_bin_kernel<B, 0, kKptMax, Keys>);
     };

@@ -52,7 +52,7 @@ def log(rank, *a):
 class Workload:
     """Device-resident inputs + a step() that performs one build."""
 
-    def __init__(self, kind, rank, n):
+    def __init__(self, kind, rank, n, world=1):
         import numpy as np
         import torch
 
@@ -78,10 +78,14 @@ class Workload:
                            "keys_per_gpu": n, "mean_key_bytes": round(total / n, 2), "bits_per_key": BPK,
                            "filters_per_gpu": 1}
             self.dtype = "u32"
-        else:  # compaction: 32 tables x 1M keys per GPU, tables t = 32*rank .. 32*rank+31
-            T, per = 32, 1_000_000
+        else:  # compaction: 32 tables x 1M keys per GPU; table t lives on GPU t // 32
+            from adlbloom import dist as D
+
+            per = 1_000_000
+            tables = D.table_shard(32 * world, world, rank)
+            T = len(tables)
             self.n = T * per
-            self.keys = torch.cat([ab.synth_keys16(per, seed=0x5EED + 32 * rank + t) for t in range(T)])
+            self.keys = torch.cat([ab.synth_keys16(per, seed=0x5EED + t) for t in tables])
             kb = np.arange(T + 1, dtype=np.uint64) * per
             self.builder = ab.SegmentedBuilder(kb, BPK)
             self.bytes_per_launch = ALGO_BYTES_PER_KEY16 * self.n
@@ -192,7 +196,7 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
-    w = Workload(args.workload, rank, args.keys)
+    w = Workload(args.workload, rank, args.keys, world)
     torch.cuda.synchronize()
     for _ in range(args.warmup):
         w.step()
@@ -206,15 +210,9 @@ def main():
     ms_a, ms_b, nb = ab.profile_collect()
 
     # RCCL: the only collective -- sum of keys built, max of elapsed time
-    stats = torch.tensor([float(w.n) * args.steps, elapsed], dtype=torch.float64, device="cuda")
-    if world > 1:
-        keys_t = stats[:1].clone()
-        dist.all_reduce(keys_t, op=dist.ReduceOp.SUM)
-        el_t = stats[1:].clone()
-        dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
-        total_keys, elapsed_max = keys_t.item(), el_t.item()
-    else:
-        total_keys, elapsed_max = stats[0].item(), stats[1].item()
+    from adlbloom import dist as D
+
+    total_keys, elapsed_max = D.reduce_throughput(float(w.n) * args.steps, elapsed, device="cuda")
 
     parity = parity_check(bm, w.n) if (rank == 0 and args.workload == "single") else None
 
