@@ -63,6 +63,8 @@ struct FilterDesc {
   uint32_t chunks;      // W
   uint32_t tiles;       // T
   FastMod mod;          // m = 8 * bitmap bytes
+  uint32_t wrap;        // 2^32 mod m (incremental positions)
+  uint32_t pad_;
 };
 
 struct BuildArgs {
@@ -75,6 +77,9 @@ struct BuildArgs {
   uint32_t xcd_remap;  // consecutive chunks / tiles on one XCD (tuning, ADL_BLOOM_XCD_REMAP)
   uint32_t nt_keys;    // pass A: non-temporal key loads (tuning, ADL_BLOOM_NT_KEYS)
   uint32_t nt_bitmap;  // pass B: non-temporal bitmap stores (tuning, ADL_BLOOM_NT_BITMAP)
+  uint32_t dyn_tiles;  // pass B: tiles from a work queue that pass A resets (ADL_BLOOM_DYN_TILES)
+  uint32_t inc_pos;    // pass A: incremental positions (ADL_BLOOM_INC_POS)
+  uint32_t stage_keys; // pass A: LDS-staged variable-length keys (16-B aligned key buffer; ADL_BLOOM_STAGE_KEYS)
   FilterDesc f[kMaxFilters];
 };
 
@@ -120,9 +125,10 @@ template <int BLOCK, int KFIX, int KPT, class Keys>
 __global__ __launch_bounds__(BLOCK) void bloom_bin_kernel(BuildArgs a, Keys keys,
                                                             uint32_t *__restrict__ pos_ws,
                                                             uint32_t *__restrict__ table_ws,
-                                                            uint32_t total_chunks) {
+                                                            uint32_t total_chunks, uint32_t *__restrict__ tile_queue) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   const int tid = threadIdx.x;
+  if (blockIdx.x == 0 && tid == 0) *tile_queue = 0;  // pass B's tile queue
   const uint32_t C = a.C;
   const uint32_t k = KFIX > 0 ? (uint32_t)KFIX : a.k;
   const uint32_t TL = a.TL;
@@ -131,6 +137,15 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin_kernel(BuildArgs a, Keys keys
   uint32_t *scratch = lds + a.hist_words;      // scan scratch (BLOCK/64 + 1, padded to 32)
   uint32_t *lpos = lds + a.hist_words + 32;    // k*C sorted tile offsets
   constexpr bool PF = KeyRegs<Keys>::kPrefetch;
+  // Variable-length keys are hashed in length order: a counting sort of the
+  // chunk's keys by length (LDS perm[]), then slot i of wave w takes the 64
+  // keys at sorted positions (i*NW + w)*64 .. +63 -- lanes of a wave hash keys
+  // of nearly equal length and every wave gets an even share of long keys.
+  constexpr bool SORT = std::is_same<Keys, KeysVar>::value;
+  constexpr int NW = BLOCK / kWave;
+  uint32_t *perm = lpos + k * C;   // C key indices (SORT)
+  uint32_t *lbin = perm + C;       // 256 length-class counters (SORT)
+  const int lane = tid & (kWave - 1), wave = tid / kWave;
 
   auto fetch = [&](uint32_t chunk, KeyRegs<Keys> (&r)[KPT]) {
     if constexpr (PF) {
@@ -175,24 +190,126 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin_kernel(BuildArgs a, Keys keys
     KeyRegs<Keys> nxt[KPT];
     if (wg + G < total_chunks) fetch(wg + G, nxt);
 
-    uint32_t h1[KPT], h2[KPT];
+    // slot i of this thread: valid[i] and the key index it hashes
+    auto slot_pos = [&](int i) -> uint32_t {
+      return SORT ? (uint32_t)((i * NW + wave) * kWave + lane) : (uint32_t)(tid + i * BLOCK);
+    };
+    uint32_t kidx[KPT];
+    if constexpr (SORT) {
+      for (uint32_t i = tid; i < 256; i += BLOCK) lbin[i] = 0;
+      __syncthreads();
+      uint32_t lb[KPT], lr[KPT];
 #pragma unroll
-    for (int i = 0; i < KPT; ++i) {
-      const uint32_t idx = tid + i * BLOCK;
-      h1[i] = h2[i] = 0;
-      if (idx < cnt) {
-        if constexpr (PF) hash16(cur[i].raw, h1[i], h2[i]);
-        else keys.hash(d.key_begin + first + idx, h1[i], h2[i]);
+      for (int i = 0; i < KPT; ++i) {
+        const uint32_t idx = tid + i * BLOCK;
+        if (idx < cnt) {
+          const uint64_t ki = d.key_begin + first + idx;
+          lb[i] = min((uint32_t)(keys.offs[ki + 1] - keys.offs[ki]) >> 2, 255u);
+          lr[i] = atomicAdd(&lbin[lb[i]], 1u);
+        }
+      }
+      __syncthreads();
+      block_excl_scan_array<BLOCK>(lbin, 256, scratch);
+#pragma unroll
+      for (int i = 0; i < KPT; ++i) {
+        const uint32_t idx = tid + i * BLOCK;
+        if (idx < cnt) perm[lbin[lb[i]] + lr[i]] = idx;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < KPT; ++i) kidx[i] = slot_pos(i) < cnt ? perm[slot_pos(i)] : 0u;
+    } else {
+#pragma unroll
+      for (int i = 0; i < KPT; ++i) kidx[i] = tid + i * BLOCK;
+    }
+
+    uint32_t h1[KPT], h2[KPT];
+    if constexpr (SORT) {
+      const uint64_t kb = d.key_begin + first;
+      const uint64_t A0 = keys.offs[kb] & ~15ull, B1 = keys.offs[kb + cnt];
+      if (a.stage_keys && B1 - A0 < (1ull << 31)) {
+        // LDS staging: the chunk's packed key bytes pass through the (still
+        // idle) position area in windows of `wcap` bytes, loaded with
+        // coalesced 16-byte loads; every key lying wholly inside the window is
+        // hashed from LDS.  The next window starts at the earliest key not yet
+        // hashed (a key straddling the window's end); a key longer than a
+        // window is hashed straight from global memory.
+        const uint32_t wcap = (4u * k * C - 16u) & ~15u;
+        uint4 *stage4 = reinterpret_cast<uint4 *>(lpos);
+        uint32_t *wmin = lbin;  // reused: window bookkeeping (the length sort is done)
+        uint32_t ks0[KPT], klen[KPT];  // key byte start (relative to A0) and length
+        uint32_t pending = 0;           // bit i: slot i still to hash
+#pragma unroll
+        for (int i = 0; i < KPT; ++i) {
+          h1[i] = h2[i] = 0;
+          if (slot_pos(i) < cnt) {
+            const uint64_t o0 = keys.offs[kb + kidx[i]];
+            ks0[i] = (uint32_t)(o0 - A0);
+            klen[i] = (uint32_t)(keys.offs[kb + kidx[i] + 1] - o0);
+            pending |= 1u << i;
+          }
+        }
+        uint64_t wb = A0;
+        // each window starts at a pending key, so it makes progress; the
+        // bound is belt and braces (left-over keys are hashed from global)
+        for (uint32_t iter = 0; wb < B1 && iter <= cnt; ++iter) {
+          const uint64_t we = min(wb + wcap, B1);
+          const uint32_t nv = (uint32_t)((we - wb) >> 4);
+          const uint4 *src = reinterpret_cast<const uint4 *>(keys.keys + wb);
+          for (uint32_t v = tid; v < nv; v += BLOCK) stage4[v] = src[v];
+          const uint32_t rem = (uint32_t)(we - wb) & 15u;  // last partial vector, bytewise
+          if (rem && (uint32_t)tid < rem)
+            reinterpret_cast<uint8_t *>(lpos)[nv * 16 + tid] = keys.keys[wb + nv * 16 + tid];
+          if (tid == 0) wmin[0] = 0xffffffffu;
+          __syncthreads();  // window staged
+          const uint32_t wlo = (uint32_t)(wb - A0), whi = (uint32_t)(we - A0);
+#pragma unroll
+          for (int i = 0; i < KPT; ++i) {
+            if (pending & (1u << i)) {
+              if (ks0[i] >= wlo && ks0[i] + klen[i] <= whi) {
+                hash_lds(lpos, ks0[i] - wlo, klen[i], h1[i], h2[i]);
+                pending &= ~(1u << i);
+              } else if (klen[i] > wcap - 16) {  // longer than any window
+                keys.hash(kb + kidx[i], h1[i], h2[i]);
+                pending &= ~(1u << i);
+              } else {
+                atomicMin(wmin, ks0[i]);
+              }
+            }
+          }
+          __syncthreads();  // window consumed; wmin = earliest pending key
+          const uint32_t nxt = wmin[0];
+          __syncthreads();  // everyone has read wmin before it is reset
+          if (nxt == 0xffffffffu) break;
+          wb = A0 + (nxt & ~15u);
+        }
+#pragma unroll
+        for (int i = 0; i < KPT; ++i)
+          if (pending & (1u << i)) keys.hash(kb + kidx[i], h1[i], h2[i]);
+      } else {
+#pragma unroll
+        for (int i = 0; i < KPT; ++i) {
+          h1[i] = h2[i] = 0;
+          if (slot_pos(i) < cnt) keys.hash(d.key_begin + first + kidx[i], h1[i], h2[i]);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < KPT; ++i) {
+        h1[i] = h2[i] = 0;
+        if (slot_pos(i) < cnt) {
+          if constexpr (PF) hash16(cur[i].raw, h1[i], h2[i]);
+          else keys.hash(d.key_begin + first + kidx[i], h1[i], h2[i]);
+        }
       }
     }
-    __syncthreads();  // hist cleared (previous iteration / prologue)
+    __syncthreads();  // hist cleared (previous iteration / prologue); staging area free
 
     constexpr int KR = KFIX > 0 ? KFIX : 1;
     uint32_t pos[KPT][KR];
 #pragma unroll
     for (int i = 0; i < KPT; ++i) {
-      const uint32_t idx = tid + i * BLOCK;
-      if (idx < cnt) {
+      if (slot_pos(i) < cnt) {
         if constexpr (KFIX > 0) {
 #pragma unroll
           for (int j = 0; j < KFIX; ++j) {
@@ -220,8 +337,7 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin_kernel(BuildArgs a, Keys keys
     // Scatter tile offsets into LDS by tile (hist now serves as the cursor).
 #pragma unroll
     for (int i = 0; i < KPT; ++i) {
-      const uint32_t idx = tid + i * BLOCK;
-      if (idx < cnt) {
+      if (slot_pos(i) < cnt) {
         if constexpr (KFIX > 0) {
           // all k cursor bumps in flight before the first dependent write
           uint32_t slot_l[KFIX];
@@ -267,16 +383,41 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin_kernel(BuildArgs a, Keys keys
 //   prefetch keys of c+2
 // so the murmur work hides under the scatter's LDS latency and the position
 // stores drain under the next count.
+// The k positions (h1 + j*h2) % m of one key, j = 0..K-1, from two
+// reductions instead of K: with d = h2 % m and W = 2^32 % m,
+//   p_{j+1} = (p_j + d - c_j * W) mod m,
+// where c_j is the carry out of the 32-bit add h_j + h2 (h_{j+1} wraps by 2^32).
+template <int K>
+__device__ __forceinline__ void positions_inc(uint32_t h1, uint32_t h2, const FastMod &mod, uint32_t wrap,
+                                              uint32_t (&pos)[K]) {
+  const uint32_t m = mod.m;
+  const uint32_t d = fastmod(h2, mod);
+  uint32_t p = fastmod(h1, mod), h = h1;
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    pos[j] = p;
+    if (j + 1 < K) {
+      const uint32_t hn = h + h2;
+      uint32_t t = p + d;
+      t = t >= m ? t - m : t;
+      if (hn < h) t = t >= wrap ? t - wrap : t + (m - wrap);
+      p = t;
+      h = hn;
+    }
+  }
+}
+
 template <int BLOCK, int K>
 __global__ __launch_bounds__(BLOCK) void bloom_bin16_kernel(BuildArgs a, Keys16 keys,
                                                               uint32_t *__restrict__ pos_ws,
                                                               uint32_t *__restrict__ table_ws,
-                                                              uint32_t total_chunks) {
+                                                              uint32_t total_chunks, uint32_t *__restrict__ tile_queue) {
   constexpr int KPT = 6;                    // keys per thread (C <= 6 * BLOCK)
   constexpr int VPT = (K * KPT + 3) / 4;    // 16-byte stores per thread per chunk, at most
   constexpr int SPI = (VPT + KPT - 1) / KPT;  // of those, per count iteration
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   const int tid = threadIdx.x;
+  if (blockIdx.x == 0 && tid == 0) *tile_queue = 0;  // pass B's tile queue
   const uint32_t C = a.C;
   const uint32_t TL = a.TL;
   const uint32_t tmask = (1u << TL) - 1u;
@@ -336,11 +477,14 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin16_kernel(BuildArgs a, Keys16 
 #pragma unroll
     for (int i = 0; i < KPT; ++i) {
       if (tid + i * BLOCK < cnt) {
+        if (a.inc_pos) {
+          positions_inc<K>(h1[i], h2[i], mod, d.wrap, pos[i]);
+        } else {
 #pragma unroll
-        for (int j = 0; j < K; ++j) {
-          pos[i][j] = fastmod(h1[i] + (uint32_t)j * h2[i], mod);
-          atomicAdd(&hist[pos[i][j] >> TL], 1u);
+          for (int j = 0; j < K; ++j) pos[i][j] = fastmod(h1[i] + (uint32_t)j * h2[i], mod);
         }
+#pragma unroll
+        for (int j = 0; j < K; ++j) atomicAdd(&hist[pos[i][j] >> TL], 1u);
       }
 #pragma unroll
       for (int sv = i * SPI; sv < (i + 1) * SPI && sv < VPT; ++sv) {
@@ -402,7 +546,7 @@ __global__ __launch_bounds__(kBlockB) void bloom_tile_kernel(BuildArgs a,
                                                              const uint32_t *__restrict__ pos_ws,
                                                              const uint32_t *__restrict__ table_ws,
                                                              uint8_t *__restrict__ bitmaps,
-                                                             uint32_t total_tiles) {
+                                                             uint32_t total_tiles, uint32_t *__restrict__ tile_queue) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   const int tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid / kWave;
   constexpr int NWAVES = kBlockB / kWave;
@@ -411,6 +555,7 @@ __global__ __launch_bounds__(kBlockB) void bloom_tile_kernel(BuildArgs a,
   const uint32_t tile_words = 1u << (TL - 5);
   uint32_t *tile = lds;                                      // 2^TL bits
   uint2 *seg = reinterpret_cast<uint2 *>(lds + tile_words);  // kSegBatch {start word, length}
+  uint32_t *qs = lds + tile_words + 2 * kSegBatch;           // tile-queue broadcast (2 words)
 
   auto fetch_rows = [&](uint32_t wg, uint32_t wb, uint32_t (&rs)[RPT], uint32_t (&re)[RPT]) {
     const FilterDesc &d = a.f[find_filter_by_tile(a, wg)];
@@ -432,23 +577,36 @@ __global__ __launch_bounds__(kBlockB) void bloom_tile_kernel(BuildArgs a,
   // consecutive tiles, so the line a tile's segment shares with its
   // neighbour's (segments of consecutive tiles are adjacent in every chunk
   // region) is fetched into one L2 once.  Speed only.
+  // Tiles come either from a work queue (dynamic: a workgroup that finishes
+  // early takes the next tile, which evens out the hot tiles) or statically,
+  // round r covering tiles [r*G, (r+1)*G) with each XCD taking G/8
+  // consecutive tiles so the line a tile's segment shares with its
+  // neighbour's is fetched into one L2 once.  Speed only, either way.
   const uint32_t G = gridDim.x;
-  const uint32_t slot =
-      (a.xcd_remap && G % 8 == 0) ? (blockIdx.x % 8) * (G / 8) + blockIdx.x / 8 : blockIdx.x;
+  uint32_t wg;
+  if (a.dyn_tiles) {
+    if (tid == 0) qs[0] = atomicAdd(tile_queue, 1u);
+    __syncthreads();
+    wg = qs[0];
+  } else {
+    wg = (a.xcd_remap && G % 8 == 0) ? (blockIdx.x % 8) * (G / 8) + blockIdx.x / 8 : blockIdx.x;
+  }
   uint32_t pre_s[RPT], pre_e[RPT];
-  if (slot < total_tiles) fetch_rows(slot, 0, pre_s, pre_e);
+  if (wg < total_tiles) fetch_rows(wg, 0, pre_s, pre_e);
 
-  for (uint32_t wg = slot; wg < total_tiles; wg += G) {
+  while (wg < total_tiles) {
     const FilterDesc &d = a.f[find_filter_by_tile(a, wg)];
     const uint32_t lt = wg - d.tile_base;
     const uint32_t W = d.chunks;
     const uint32_t pos_base = (uint32_t)d.pos_base;
 
+    if (a.dyn_tiles && tid == 0) qs[1] = atomicAdd(tile_queue, 1u);
     uint4 *t4w = reinterpret_cast<uint4 *>(tile);
     for (uint32_t i = tid; i < tile_words / 4; i += kBlockB) t4w[i] = make_uint4(0, 0, 0, 0);
+    __syncthreads();  // tile zeroed (also when W == 0); next tile index published
+    const uint32_t next = a.dyn_tiles ? qs[1] : wg + G;
     // an empty filter (no chunks) has no batch to prefetch the next tile from
-    if (W == 0 && wg + G < total_tiles) fetch_rows(wg + G, 0, pre_s, pre_e);
-    __syncthreads();  // tile zeroed (also when W == 0)
+    if (W == 0 && next < total_tiles) fetch_rows(next, 0, pre_s, pre_e);
 
     for (uint32_t wb = 0; wb < W; wb += kSegBatch) {
       const uint32_t nw = min((uint32_t)kSegBatch, W - wb);
@@ -465,7 +623,7 @@ __global__ __launch_bounds__(kBlockB) void bloom_tile_kernel(BuildArgs a,
         if (i < nw) seg[i] = make_uint2(pos_base + (wb + i) * a.cap + rs[r], re[r] - rs[r]);
       }
       __syncthreads();  // segment list ready
-      if (wb + kSegBatch >= W && wg + G < total_tiles) fetch_rows(wg + G, 0, pre_s, pre_e);
+      if (wb + kSegBatch >= W && next < total_tiles) fetch_rows(next, 0, pre_s, pre_e);
 
       const uint32_t Q = nw > (uint32_t)wave ? (nw - wave + NWAVES - 1) / NWAVES : 0;
       struct Stage {
@@ -534,6 +692,7 @@ __global__ __launch_bounds__(kBlockB) void bloom_tile_kernel(BuildArgs a,
       for (uint32_t i = tid; i < (uint32_t)(nbytes >> 4); i += kBlockB) out4[i] = t4[i];
     }
     __syncthreads();  // every lane has read the tile before the next one is zeroed
+    wg = next;
   }
 }
 
@@ -642,7 +801,11 @@ int make_plan(const uint64_t *counts, uint32_t nf, int32_t bpk, Plan &p) {
   const uint32_t grid_a_max = bpc * cus;
   const uint32_t kpt = k == 6 ? 6 : kKptMax;
   const uint32_t lds_words_a = kLdsWordsPerCu / bpc - (bpc == 1 ? 256 : 0);
-  const uint32_t cmax = std::min<uint32_t>(block_a * kpt, (lds_words_a - hist_words - 32) / k) & ~3u;
+  // LDS: tile counters + scan scratch + k*C positions + C key indices and 256
+  // length classes (the length sort of variable-length keys; reserved for every
+  // key shape so the workspace size does not depend on it)
+  const uint32_t cmax =
+      std::min<uint32_t>(block_a * kpt, (lds_words_a - hist_words - 32 - 256) / (k + 1)) & ~3u;
   if (cmax < 4) return ADL_ERR_TOO_LARGE;
   const uint64_t wmin = (total_n + cmax - 1) / cmax;
   uint32_t C;
@@ -658,6 +821,9 @@ int make_plan(const uint64_t *counts, uint32_t nf, int32_t bpk, Plan &p) {
   p.a.xcd_remap = env_flag("ADL_BLOOM_XCD_REMAP", 1);
   p.a.nt_keys = env_flag("ADL_BLOOM_NT_KEYS", 1);
   p.a.nt_bitmap = env_flag("ADL_BLOOM_NT_BITMAP", 1);
+  p.a.dyn_tiles = env_flag("ADL_BLOOM_DYN_TILES", 0);
+  p.a.inc_pos = env_flag("ADL_BLOOM_INC_POS", 0);
+  p.a.stage_keys = env_flag("ADL_BLOOM_STAGE_KEYS", 1);
   p.a.k = k;
   p.a.C = C;
   p.a.TL = TL;
@@ -676,6 +842,7 @@ int make_plan(const uint64_t *counts, uint32_t nf, int32_t bpk, Plan &p) {
     d.tiles = (uint32_t)(((uint64_t)m + (1ull << TL) - 1) >> TL);
     if (d.tiles + 1 > kHistMax) return ADL_ERR_TOO_LARGE;
     d.mod = adl_host::make_fastmod(m);
+    d.wrap = (uint32_t)((1ull << 32) % m);
     d.chunk_base = chunk;
     d.tile_base = tile;
     d.pos_base = pos;
@@ -693,8 +860,8 @@ int make_plan(const uint64_t *counts, uint32_t nf, int32_t bpk, Plan &p) {
   p.pos_words = adl_host::round_up(pos, 64);
   p.table_words = adl_host::round_up(tab + kTablePad, 64);
   p.ws_bytes = (p.pos_words + p.table_words) * 4 + 256;
-  p.lds_a = (size_t)(hist_words + 32 + k * C) * 4;
-  p.lds_b = (size_t)((1u << (TL - 5)) + 2 * kSegBatch) * 4;
+  p.lds_a = (size_t)(hist_words + 32 + (k + 1) * C + 256) * 4;
+  p.lds_b = (size_t)((1u << (TL - 5)) + 2 * kSegBatch + 4) * 4;
   p.grid_a = std::min<uint32_t>(p.total_chunks, grid_a_max);
   p.block_a = block_a;
   p.depth = env_u32("ADL_BLOOM_DEPTH", kDepthB);
@@ -731,6 +898,7 @@ template <class Keys>
 int launch_binned(const Plan &p, Keys keys, uint8_t *d_bitmaps, void *ws, hipStream_t st) {
   uint32_t *pos_ws = reinterpret_cast<uint32_t *>(ws);
   uint32_t *tab_ws = pos_ws + p.pos_words;
+  uint32_t *queue = tab_ws + p.table_words;  // pass B tile queue (inside the +256 B slack)
   hipEvent_t *ev = prof_slot();
   if (ev) ADL_HIP_TRY(hipEventRecord(ev[0], st));
   if (p.total_chunks) {
@@ -738,7 +906,7 @@ int launch_binned(const Plan &p, Keys keys, uint8_t *d_bitmaps, void *ws, hipStr
       ADL_HIP_TRY(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                                       (int)p.lds_a));
       hipLaunchKernelGGL(kern, dim3(p.grid_a), dim3(p.block_a), p.lds_a, st, p.a, keys, pos_ws, tab_ws,
-                         p.total_chunks);
+                         p.total_chunks, queue);
       ADL_HIP_TRY(hipGetLastError());
       return ADL_OK;
     };
@@ -757,15 +925,18 @@ int launch_binned(const Plan &p, Keys keys, uint8_t *d_bitmaps, void *ws, hipStr
   if (ev) ADL_HIP_TRY(hipEventRecord(ev[1], st));
   auto go_b = [&](auto kern) -> int {
     ADL_HIP_TRY(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)p.lds_b));
-    hipLaunchKernelGGL(kern, dim3(p.grid_b), dim3(kBlockB), p.lds_b, st, p.a, (const uint32_t *)pos_ws,
-                       (const uint32_t *)tab_ws, d_bitmaps, p.total_tiles);
+    BuildArgs ab = p.a;
+    if (!p.total_chunks) ab.dyn_tiles = 0;  // no pass A ran to reset the queue
+    hipLaunchKernelGGL(kern, dim3(p.grid_b), dim3(kBlockB), p.lds_b, st, ab, (const uint32_t *)pos_ws,
+                       (const uint32_t *)tab_ws, d_bitmaps, p.total_tiles, queue);
     ADL_HIP_TRY(hipGetLastError());
     return ADL_OK;
   };
   int rcb;
-  if (p.depth <= 8) rcb = go_b(bloom_tile_kernel<8>);
-  else if (p.depth <= 12) rcb = go_b(bloom_tile_kernel<12>);
-  else rcb = go_b(bloom_tile_kernel<16>);
+  if (p.depth <= 4) rcb = go_b(bloom_tile_kernel<4>);
+  else if (p.depth <= 6) rcb = go_b(bloom_tile_kernel<6>);
+  else if (p.depth <= 8) rcb = go_b(bloom_tile_kernel<8>);
+  else rcb = go_b(bloom_tile_kernel<12>);
   if (rcb) return rcb;
   if (ev) ADL_HIP_TRY(hipEventRecord(ev[2], st));
   return ADL_OK;
@@ -822,6 +993,7 @@ int build_groups(const uint8_t *d_keys, const uint64_t *d_offsets, uint32_t key_
     if (ws) ws = reinterpret_cast<void *>(adl_host::round_up(reinterpret_cast<uintptr_t>(ws), 256));
     if (d_offsets) {
       KeysVar keys{d_keys, d_offsets};
+      if (reinterpret_cast<uintptr_t>(d_keys) % 16) p.a.stage_keys = 0;  // staging loads are 16-byte
       rc = atomic ? launch_atomic(p, keys, d_bitmaps, st) : launch_binned(p, keys, d_bitmaps, ws, st);
     } else if (key_stride == 16 && (reinterpret_cast<uintptr_t>(d_keys) % 16) == 0) {
       Keys16 keys{reinterpret_cast<const uint4 *>(d_keys)};

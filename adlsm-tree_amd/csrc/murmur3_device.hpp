@@ -92,14 +92,25 @@ __device__ __forceinline__ uint32_t load_u32_unaligned(const uint8_t *p) {
 }
 
 // Both seeds of an arbitrary-length key at byte pointer p (any alignment).
+// The block words are independent of the hash state, so they are loaded 8 at
+// a time (one memory round trip per 32 key bytes) and then mixed in order.
 __device__ __forceinline__ void hash_bytes(const uint8_t *p, uint32_t len, uint32_t seed_a,
                                            uint32_t seed_b, uint32_t &ha, uint32_t &hb) {
   uint32_t a = seed_a, b = seed_b;
   const uint32_t nblk = len >> 2;
-  for (uint32_t i = 0; i < nblk; ++i) {
-    const uint32_t w = quirk_word(load_u32_unaligned(p + 4 * i));
-    a = mix_block(a, w);
-    b = mix_block(b, w);
+  constexpr uint32_t U = 8;
+  for (uint32_t i = 0; i < nblk; i += U) {
+    uint32_t w[U];
+#pragma unroll
+    for (uint32_t u = 0; u < U; ++u) w[u] = i + u < nblk ? load_u32_unaligned(p + 4 * (i + u)) : 0u;
+#pragma unroll
+    for (uint32_t u = 0; u < U; ++u) {
+      if (i + u < nblk) {
+        const uint32_t q = quirk_word(w[u]);
+        a = mix_block(a, q);
+        b = mix_block(b, q);
+      }
+    }
   }
   const uint32_t rem = len & 3u;
   if (rem) {
@@ -107,6 +118,33 @@ __device__ __forceinline__ void hash_bytes(const uint8_t *p, uint32_t len, uint3
     uint32_t raw = t[0];
     if (rem >= 2) raw |= (uint32_t)t[1] << 8;
     if (rem >= 3) raw |= (uint32_t)t[2] << 16;
+    const uint32_t k1 = tail_word(raw, rem);
+    a = mix_tail(a, k1);
+    b = mix_tail(b, k1);
+  }
+  ha = fmix(a, len);
+  hb = fmix(b, len);
+}
+
+// Both seeds of a key staged in LDS at byte offset `off` of `stage` (any
+// alignment): one aligned ds_read_b32 per block plus v_alignbyte_b32 with the
+// previous word.  Reads up to 4 bytes past the key's end (callers keep slack).
+__device__ __forceinline__ void hash_lds(const uint32_t *stage, uint32_t off, uint32_t len,
+                                         uint32_t &ha, uint32_t &hb) {
+  uint32_t a = kSeed1, b = kSeed2;
+  const uint32_t nblk = len >> 2, sh = off & 3u;
+  uint32_t wi = off >> 2;
+  uint32_t lo = stage[wi];
+  for (uint32_t i = 0; i < nblk; ++i) {
+    const uint32_t hi = stage[++wi];
+    const uint32_t q = quirk_word(__builtin_amdgcn_alignbyte(hi, lo, sh));
+    a = mix_block(a, q);
+    b = mix_block(b, q);
+    lo = hi;
+  }
+  const uint32_t rem = len & 3u;
+  if (rem) {
+    const uint32_t raw = __builtin_amdgcn_alignbyte(stage[wi + 1], lo, sh);
     const uint32_t k1 = tail_word(raw, rem);
     a = mix_tail(a, k1);
     b = mix_tail(b, k1);
