@@ -36,7 +36,7 @@ EXPORTS = (
     "adl_bloom_filter_set_device_view", "adl_bloom_filter_set_destroy",
     "adl_bloom_murmur3_device", "adl_bloom_murmur3", "adl_synth_keys16_device",
     "adl_synth_varlen_lengths_device", "adl_synth_varlen_fill_device",
-    "adl_bloom_profile_enable", "adl_bloom_profile_collect",
+    "adl_bloom_profile_enable", "adl_bloom_profile_collect", "adl_synth_probe_queries_device",
 )
 
 _LIB = None
@@ -81,6 +81,7 @@ def lib() -> ctypes.CDLL:
         "adl_synth_keys16_device": (ctypes.c_int, [vp, u64, u64, u64, vp]),
         "adl_synth_varlen_lengths_device": (ctypes.c_int, [vp, u64, u64, ctypes.c_double, vp]),
         "adl_synth_varlen_fill_device": (ctypes.c_int, [vp, u64, u64, vp]),
+        "adl_synth_probe_queries_device": (ctypes.c_int, [vp, vp, vp, u64, u64, u64, u32, u64, u64, vp]),
         "adl_bloom_profile_enable": (ctypes.c_int, [u32]),
         "adl_bloom_profile_collect": (ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(u32)]),
     }
@@ -372,3 +373,17 @@ def synth_varlen(n: int, seed: int = 0x5EED, zipf_s: float = 1.1, device="cuda",
     _check(lib().adl_synth_varlen_fill_device(_dptr(data), seed, total, _stream(stream)),
            "adl_synth_varlen_fill_device")
     return data, offs  # int64 storage, read as uint64 offsets by the C-ABI
+
+
+def synth_probe_queries(n: int, seed: int = 0xFEED, q0: int = 0, num_tables: int = 256,
+                        table_seed0: int = 0x5EED, keys_per_table: int = 1_000_000, device="cuda", stream=None):
+    """Probe queries of BASELINE.json configs[4] on the device: (keys (n,16) u8, filter_id int32
+    (read as uint32), member u8) -- see adl_synth_probe_queries_device."""
+    torch = _torch()
+    keys = torch.empty((max(n, 1), 16), dtype=torch.uint8, device=device)
+    fid = torch.empty(max(n, 1), dtype=torch.int32, device=device)
+    member = torch.empty(max(n, 1), dtype=torch.uint8, device=device)
+    _check(lib().adl_synth_probe_queries_device(_dptr(keys), _dptr(fid), _dptr(member), seed, q0, n, num_tables,
+                                                table_seed0, keys_per_table, _stream(stream)),
+           "adl_synth_probe_queries_device")
+    return keys[:n], fid[:n], member[:n]

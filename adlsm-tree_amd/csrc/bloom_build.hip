@@ -746,19 +746,6 @@ uint32_t env_u32(const char *name, uint32_t dflt) {
   return e ? (uint32_t)atoi(e) : dflt;
 }
 
-// Compute units of the current device (256 on MI355X), queried once.
-uint32_t device_cus() {
-  static std::once_flag once;
-  static uint32_t cus = 256;
-  std::call_once(once, [] {
-    int dev = 0, v = 0;
-    if (hipGetDevice(&dev) == hipSuccess &&
-        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0)
-      cus = (uint32_t)v;
-  });
-  return cus;
-}
-
 int make_plan(const uint64_t *counts, uint32_t nf, int32_t bpk, Plan &p) {
   if (nf == 0 || nf > (uint32_t)kMaxFilters || bpk < 0) return ADL_ERR_INVALID_ARG;
   memset(&p.a, 0, sizeof(p.a));
@@ -795,7 +782,7 @@ int make_plan(const uint64_t *counts, uint32_t nf, int32_t bpk, Plan &p) {
   // one workgroup's hashing with the other's LDS sort; 1 x 1024 threads per
   // CU doubles the chunk, so pass B gathers half as many, twice as long
   // segments.
-  const uint32_t cus = device_cus();
+  const uint32_t cus = adl_host::device_cus();
   const uint32_t bpc = env_u32("ADL_BLOOM_A_WGS_PER_CU", 1) == 2 ? 2 : 1;
   const uint32_t block_a = bpc == 1 ? 1024 : 512;
   const uint32_t grid_a_max = bpc * cus;

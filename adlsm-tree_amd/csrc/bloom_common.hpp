@@ -2,6 +2,8 @@
 // libadlbloom.so: status handling, key-set views, block scans.
 #pragma once
 #include <hip/hip_runtime.h>
+
+#include <mutex>
 #include <stdint.h>
 
 #include "../../include/adl_bloom.h"
@@ -136,6 +138,19 @@ inline adl_dev::FastMod make_fastmod(uint32_t m) {
   f.magic = (uint32_t)((((1ull << 32) * ((1ull << l) - m)) / m) + 1ull);
   f.shift = l - 1;
   return f;
+}
+
+// Compute units of the current device (256 on MI355X), queried once.
+inline uint32_t device_cus() {
+  static std::once_flag once;
+  static uint32_t cus = 256;
+  std::call_once(once, [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0)
+      cus = (uint32_t)v;
+  });
+  return cus;
 }
 
 inline int num_probes(int32_t bpk) {

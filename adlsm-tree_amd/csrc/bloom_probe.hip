@@ -5,7 +5,8 @@
 // for a batch: m = bitmap_bytes*8 (:50), the same h1 + j*h2 positions as the
 // build, "absent" at the first clear bit (:54-59).  One query per lane; the key
 // load is coalesced, the k bitmap reads are random byte loads that stop at the
-// first clear bit (the same early exit as the reference).
+// first clear bit (the same early exit as the reference), issued a few at a
+// time so that independent reads overlap.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string.h>
@@ -22,6 +23,33 @@ namespace {
 
 constexpr int kBlockP = 256;
 
+constexpr uint32_t kProbeFirst = 2;      // bitmap reads in the first round of a query
+constexpr uint32_t kProbeGroup = 4;      // ... and in every later round
+constexpr uint32_t kLdsFilters = 4096;   // per-filter divisor table kept in LDS up to this many
+
+// The k bitmap reads of one query, issued in rounds (kProbeFirst, then
+// kProbeGroup at a time) so independent random reads overlap while a clear bit
+// still ends the query early, like the reference's loop
+// (src/filter_block.cpp:54-59).  The answer does not depend on the grouping.
+__device__ __forceinline__ uint8_t probe_bits(const uint8_t *__restrict__ bm, uint32_t h1, uint32_t h2,
+                                              uint32_t k, const FastMod &mod) {
+  uint32_t j = 0, group = kProbeFirst;
+  while (j < k) {
+    uint32_t all = 1;
+#pragma unroll
+    for (uint32_t g = 0; g < kProbeGroup; ++g) {
+      if (g < group && j + g < k) {
+        const uint32_t p = fastmod(h1 + (j + g) * h2, mod);
+        all &= (uint32_t)(bm[p >> 3] >> (p & 7));
+      }
+    }
+    if (!(all & 1u)) return 0;
+    j += group;
+    group = kProbeGroup;
+  }
+  return 1;
+}
+
 template <class Keys>
 __global__ __launch_bounds__(kBlockP) void bloom_probe_kernel(Keys keys, uint64_t n, uint32_t k,
                                                               FastMod mod,
@@ -31,25 +59,32 @@ __global__ __launch_bounds__(kBlockP) void bloom_probe_kernel(Keys keys, uint64_
        i += (uint64_t)gridDim.x * kBlockP) {
     uint32_t h1, h2;
     keys.hash(i, h1, h2);
-    uint8_t hit = 1;
-    for (uint32_t j = 0; j < k; ++j) {
-      const uint32_t p = fastmod(h1 + j * h2, mod);
-      if (!((bitmap[p >> 3] >> (p & 7)) & 1u)) {
-        hit = 0;
-        break;
-      }
-    }
-    out[i] = hit;
+    out[i] = probe_bits(bitmap, h1, h2, k, mod);
   }
 }
 
-// Multi-filter probe: per-query divisor, so the remainder is the hardware-free
-// 32-bit `%` sequence instead of a launch-constant magic multiply.
+// Multi-filter probe: query i against filter fid[i] (or uniform_f).  Each
+// filter has its own divisor m = 8 * bitmap bytes; the magic-multiply
+// constants of up to kLdsFilters filters are built once per workgroup into
+// LDS (dynamic, 8 B per filter), beyond that per query.
+struct ModLds {
+  uint32_t magic, shift_pow2;  // shift | pow2 << 8
+};
+
 template <class Keys>
 __global__ __launch_bounds__(kBlockP) void bloom_probe_multi_kernel(
     Keys keys, uint64_t n, uint32_t k, const uint32_t *__restrict__ fid, uint32_t uniform_f,
     uint32_t nf, const uint8_t *__restrict__ bitmaps, const uint64_t *__restrict__ boff,
     uint8_t *__restrict__ out) {
+  extern __shared__ ModLds lmod[];
+  const bool lds_tab = nf <= kLdsFilters;
+  if (lds_tab) {
+    for (uint32_t f = threadIdx.x; f < nf; f += kBlockP) {
+      const FastMod fm = fastmod_for((uint32_t)((boff[f + 1] - boff[f]) * 8));
+      lmod[f] = ModLds{fm.magic, fm.shift | (fm.pow2 << 8)};
+    }
+    __syncthreads();
+  }
   for (uint64_t i = blockIdx.x * (uint64_t)kBlockP + threadIdx.x; i < n;
        i += (uint64_t)gridDim.x * kBlockP) {
     const uint32_t f = fid ? fid[i] : uniform_f;  // fid == nullptr: every query -> uniform_f
@@ -57,13 +92,17 @@ __global__ __launch_bounds__(kBlockP) void bloom_probe_multi_kernel(
     if (f < nf) {
       const uint64_t b0 = boff[f], b1 = boff[f + 1];
       const uint32_t m = (uint32_t)((b1 - b0) * 8);
-      const uint8_t *bm = bitmaps + b0;
-      uint32_t h1, h2;
-      keys.hash(i, h1, h2);
-      hit = m != 0;
-      for (uint32_t j = 0; j < k && hit; ++j) {
-        const uint32_t p = (h1 + j * h2) % m;
-        if (!((bm[p >> 3] >> (p & 7)) & 1u)) hit = 0;
+      if (m != 0) {
+        FastMod mod;
+        if (lds_tab) {
+          const ModLds e = lmod[f];
+          mod = FastMod{m, e.magic, e.shift_pow2 & 0xffu, e.shift_pow2 >> 8};
+        } else {
+          mod = fastmod_for(m);
+        }
+        uint32_t h1, h2;
+        keys.hash(i, h1, h2);
+        hit = probe_bits(bitmaps + b0, h1, h2, k, mod);
       }
     }
     out[i] = hit;
@@ -116,6 +155,30 @@ __global__ __launch_bounds__(256) void synth_keys16_kernel(uint4 *__restrict__ o
   }
 }
 
+__global__ __launch_bounds__(256) void synth_probe_kernel(uint4 *__restrict__ keys, uint32_t *__restrict__ fid,
+                                                          uint8_t *__restrict__ member, uint64_t seed, uint64_t q0,
+                                                          uint64_t n, uint32_t tables, uint64_t tseed0,
+                                                          uint64_t per_table) {
+  for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+    const uint64_t c = 4 * (q0 + i);
+    const uint64_t r0 = splitmix_at(seed, c + 1), r1 = splitmix_at(seed, c + 2);
+    const uint32_t t = (uint32_t)(r0 % tables);
+    uint64_t a, b;
+    const bool ins = (r1 & 1) && per_table;
+    if (ins) {
+      const uint64_t j = (r1 >> 1) % per_table;
+      a = splitmix_at(tseed0 + t, 2 * j + 1);
+      b = splitmix_at(tseed0 + t, 2 * j + 2);
+    } else {
+      a = splitmix_at(seed, c + 3);
+      b = splitmix_at(seed, c + 4);
+    }
+    keys[i] = make_uint4((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32));
+    fid[i] = t;
+    if (member) member[i] = ins;
+  }
+}
+
 constexpr int kZipfR = 249;  // lengths 8 .. 256
 
 __global__ __launch_bounds__(256) void synth_lengths_kernel(uint32_t *__restrict__ len, uint64_t seed,
@@ -148,8 +211,12 @@ __global__ __launch_bounds__(256) void synth_fill_kernel(uint64_t *__restrict__ 
     out[i] = splitmix_at(seed, i + 1);
 }
 
-inline uint32_t grid_for(uint64_t n, int block) {
-  return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n + block - 1) / block, 256ull * 64));
+// Grid-stride launches: enough workgroups to cover n, at most blocks_per_cu
+// per CU (the multi-filter probe amortises a per-workgroup table over many
+// queries, so it asks for a persistent-sized grid).
+inline uint32_t grid_for(uint64_t n, int block, uint32_t blocks_per_cu = 64) {
+  return (uint32_t)std::max<uint64_t>(
+      1, std::min<uint64_t>((n + block - 1) / block, (uint64_t)adl_host::device_cus() * blocks_per_cu));
 }
 
 template <class F>
@@ -195,8 +262,9 @@ int probe_multi(const uint8_t *d_keys, const uint64_t *d_offsets, uint64_t n, ui
   if (!d_offsets && key_stride == 0) return ADL_ERR_INVALID_ARG;
   const uint32_t k = (uint32_t)adl_host::num_probes(bits_per_key);
   return dispatch_keys(d_keys, d_offsets, key_stride, [&](auto keys) -> int {
-    hipLaunchKernelGGL(bloom_probe_multi_kernel<decltype(keys)>, dim3(grid_for(n, kBlockP)),
-                       dim3(kBlockP), 0, st, keys, n, k, d_filter_id, uniform_f, num_filters,
+    const size_t lds = num_filters <= kLdsFilters ? (size_t)num_filters * sizeof(ModLds) : 0;
+    hipLaunchKernelGGL(bloom_probe_multi_kernel<decltype(keys)>, dim3(grid_for(n, kBlockP, 8)),
+                       dim3(kBlockP), lds, st, keys, n, k, d_filter_id, uniform_f, num_filters,
                        d_bitmaps, d_bitmap_off, d_out);
     ADL_HIP_TRY(hipGetLastError());
     return ADL_OK;
@@ -314,6 +382,19 @@ int adl_synth_varlen_fill_device(uint8_t *d_out, uint64_t seed, uint64_t total_b
   const uint64_t words = (total_bytes + 7) / 8;  // caller allocates round_up(total_bytes, 8)
   hipLaunchKernelGGL(synth_fill_kernel, dim3(grid_for(words, 256)), dim3(256), 0, (hipStream_t)stream,
                      reinterpret_cast<uint64_t *>(d_out), seed, words);
+  ADL_HIP_TRY(hipGetLastError());
+  return ADL_OK;
+}
+
+int adl_synth_probe_queries_device(uint8_t *d_keys, uint32_t *d_filter_id, uint8_t *d_member,
+                                   uint64_t seed, uint64_t q0, uint64_t n, uint32_t num_tables,
+                                   uint64_t table_seed0, uint64_t keys_per_table, void *stream) {
+  if (n == 0) return ADL_OK;
+  if (!d_keys || !d_filter_id || num_tables == 0 || reinterpret_cast<uintptr_t>(d_keys) % 16)
+    return ADL_ERR_INVALID_ARG;
+  hipLaunchKernelGGL(synth_probe_kernel, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream,
+                     reinterpret_cast<uint4 *>(d_keys), d_filter_id, d_member, seed, q0, n, num_tables,
+                     table_seed0, keys_per_table);
   ADL_HIP_TRY(hipGetLastError());
   return ADL_OK;
 }

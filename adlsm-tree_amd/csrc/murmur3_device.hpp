@@ -160,6 +160,22 @@ struct FastMod {
   uint32_t m, magic, shift, pow2;
 };
 
+// Device-side construction (same values as adl_host::make_fastmod); for
+// per-filter divisors that are only known on the device.
+__device__ __forceinline__ FastMod fastmod_for(uint32_t m) {
+  FastMod f;
+  f.m = m;
+  if ((m & (m - 1u)) == 0u) {
+    f.pow2 = 1; f.magic = 0; f.shift = 0;
+    return f;
+  }
+  const uint32_t l = 32u - __clz(m - 1u);  // ceil(log2 m), m >= 3
+  f.pow2 = 0;
+  f.magic = (uint32_t)((((1ull << 32) * ((1ull << l) - m)) / m) + 1ull);
+  f.shift = l - 1u;
+  return f;
+}
+
 __device__ __forceinline__ uint32_t fastmod(uint32_t h, const FastMod &d) {
   if (d.pow2) return h & (d.m - 1u);
   const uint32_t t = __umulhi(h, d.magic);

@@ -11,6 +11,9 @@ pass A (hash + bin) and pass B (LDS tile OR + bitmap write).  Workloads:
   compaction  32 SSTables x 1M x 16 B keys per GPU in one segmented build
               (configs[3]: 256 tables over 8 GPUs).
   varlen      10M variable-length keys (8-256 B, Zipf(1.1) lengths) per GPU (configs[2]).
+  probe       100M 16 B queries against 256 device-resident 1M-key filters (configs[4]);
+              filters t -> GPU t // (256/N), each GPU probes the queries of its own
+              filters (strong scaling: the 100M total is fixed).
 
 Multi-GPU: one process per GPU (torch.distributed.run); no collective on the
 data path -- each rank owns whole filters.  RCCL reduces only the key counter
@@ -28,6 +31,8 @@ sys.path.insert(0, os.path.join(ROOT, "adlsm-tree_amd"))
 
 BPK = 10
 ALGO_BYTES_PER_KEY16 = 26  # 16 B key read + (n*bpk+7)/n ~ 10 B bitmap write
+ALGO_BYTES_PER_QUERY = 21  # 16 B query + 4 B filter id + 1 B result
+PROBE_TABLES, PROBE_KEYS_PER_TABLE = 256, 1_000_000
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 
 
@@ -36,8 +41,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", default="single", choices=["single", "compaction", "varlen"])
+    ap.add_argument("--workload", default="single", choices=["single", "compaction", "varlen", "probe"])
     ap.add_argument("--keys", type=int, default=10_000_000, help="keys per filter (single/varlen)")
+    ap.add_argument("--queries", type=int, default=100_000_000, help="total probe queries (probe)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget")
@@ -52,7 +58,7 @@ def log(rank, *a):
 class Workload:
     """Device-resident inputs + a step() that performs one build."""
 
-    def __init__(self, kind, rank, n, world=1):
+    def __init__(self, kind, rank, n, world=1, queries=0):
         import numpy as np
         import torch
 
@@ -78,6 +84,8 @@ class Workload:
                            "keys_per_gpu": n, "mean_key_bytes": round(total / n, 2), "bits_per_key": BPK,
                            "filters_per_gpu": 1}
             self.dtype = "u32"
+        elif kind == "probe":
+            self._init_probe(rank, world, queries)
         else:  # compaction: 32 tables x 1M keys per GPU; table t lives on GPU t // 32
             from adlbloom import dist as D
 
@@ -93,29 +101,200 @@ class Workload:
                            "keys_per_gpu": self.n, "key_bytes": 16, "bits_per_key": BPK, "filters_per_gpu": T}
             self.dtype = "u32"
 
+    def _init_probe(self, rank, world, queries):
+        """configs[4]: 256 tables x 1M keys (this rank's share built on the device in
+        segmented builds of 32 tables), compacted to exact-length bitmaps; the
+        global query stream is generated on the device and this rank keeps the
+        queries of the filters it owns."""
+        import numpy as np
+        import torch
+
+        import adlbloom as ab
+        from adlbloom import dist as D
+
+        per = PROBE_KEYS_PER_TABLE
+        tables = D.table_shard(PROBE_TABLES, world, rank)
+        self.tables = tables
+        pieces, sizes = [], []
+        for g0 in range(tables.start, tables.stop, 32):
+            grp = range(g0, min(g0 + 32, tables.stop))
+            keys = torch.cat([ab.synth_keys16(per, seed=0x5EED + t) for t in grp])
+            bms, boff, sz = ab.build_segmented(keys, np.arange(len(grp) + 1, dtype=np.uint64) * per)
+            pieces += [bms[int(o):int(o) + int(z)] for o, z in zip(boff, sz)]
+            sizes += [int(z) for z in sz]
+            del keys
+        self.bitmaps = torch.cat(pieces)
+        del pieces
+        off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.uint64)
+        self.bitmap_off_host = off
+        self.bitmap_off = torch.from_numpy(off.view(np.int64)).cuda()
+        # the global query stream in slices; keep this rank's queries (local filter ids)
+        ks, fs, ms = [], [], []
+        step = 25_000_000
+        for q0 in range(0, queries, step):
+            k, f, m = ab.synth_probe_queries(min(step, queries - q0), q0=q0, num_tables=PROBE_TABLES,
+                                             keys_per_table=per)
+            sel = (f >= tables.start) & (f < tables.stop)
+            ks.append(k[sel])
+            fs.append(f[sel] - tables.start)
+            ms.append(m[sel])
+        self.keys, self.fid, self.member = torch.cat(ks), torch.cat(fs), torch.cat(ms)
+        del ks, fs, ms
+        self.n = int(self.keys.shape[0])
+        self.total_queries = queries
+        self.bytes_per_launch = ALGO_BYTES_PER_QUERY * self.n
+        self.config = {"workload": f"probe: {queries // 1_000_000}M x 16B queries vs {PROBE_TABLES} device-resident "
+                                   f"filters of {per // 1_000_000}M keys (50% inserted keys)",
+                       "queries_total": queries, "queries_this_gpu": self.n, "filters_total": PROBE_TABLES,
+                       "filters_per_gpu": len(tables), "keys_per_filter": per, "bits_per_key": BPK}
+        self.dtype = "u32"
+
     def step(self):
+        if self.kind == "probe":
+            import adlbloom as ab
+
+            return ab.probe_multi(self.keys, self.fid, self.bitmaps, self.bitmap_off)
         if self.kind == "varlen":
             return self.builder.build(self.keys, self.offs)
         return self.builder.build(self.keys)
 
 
-def cpu_baseline(budget_s):
-    """The oracle's C restatement of BloomFilter::Keys2Block (single thread,
-    gcc -O2) on the same 10M x 16 B SplitMix64 workload, repeated within budget."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import oracle as O
+def _cpu_cores():
+    """Host threads for the multi-filter CPU baselines: this process's CPU share,
+    capped at 16 (the GPU box's share per GPU)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))
 
-    n = 10_000_000
-    keys = O.splitmix_keys16(0x5EED, n)
+
+def _timed_reps(fn, budget_s, max_reps=20):
     reps, t_total = 0, 0.0
-    while reps < 20 and t_total < budget_s:
+    while reps < max_reps and t_total < budget_s:
         t0 = time.perf_counter()
-        O.keys2block(keys, bits_per_key=BPK)
+        fn()
         t_total += time.perf_counter() - t0
         reps += 1
+    return reps, t_total
+
+
+def cpu_baseline(budget_s, workload="single", w=None):
+    """The oracle's C restatement of the reference path (gcc -O2) on the same
+    synthetic inputs, timed on this host: BloomFilter::Keys2Block
+    (src/filter_block.cpp:9-33) single-threaded for one filter, one filter per
+    thread for the 32-table compaction shard, and IsKeyExists
+    (src/filter_block.cpp:49-62) over query slices per thread for the probe."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from concurrent.futures import ThreadPoolExecutor
+
+    import numpy as np
+
+    import oracle as O
+
+    if workload == "varlen":
+        data = w.keys.cpu().numpy()
+        offs = w.offs.cpu().numpy().view(np.uint64)
+        n = len(offs) - 1
+        reps, t = _timed_reps(lambda: O.keys2block(data, offsets=offs, bits_per_key=BPK), budget_s)
+        return {"value": round(n * reps / t / 1e6, 3), "unit": "Mkeys/s", "cores": 1, "kind": "port",
+                "sample": f"{reps} x full {n // 1_000_000}M var-len-key build (same keys as the GPU run), "
+                          f"oracle_keys2block (C restatement of src/filter_block.cpp:9-33, gcc -O2), {t:.1f} s"}
+    if workload == "compaction":
+        per, T = 1_000_000, 32
+        cores = _cpu_cores()
+        tables = [O.splitmix_keys16(0x5EED + t, per) for t in range(T)]
+        with ThreadPoolExecutor(cores) as ex:
+            def run():
+                list(ex.map(lambda k: O.keys2block(k, bits_per_key=BPK), tables))
+            reps, t = _timed_reps(run, budget_s)
+        return {"value": round(T * per * reps / t / 1e6, 3), "unit": "Mkeys/s", "cores": cores, "kind": "port",
+                "sample": f"{reps} x 32 tables x 1M x 16B keys (rank-0 shard), one filter per thread on "
+                          f"{cores} threads, oracle_keys2block (gcc -O2), {t:.1f} s"}
+    if workload == "probe":
+        cores = _cpu_cores()
+        ns = min(w.n, 2_000_000)
+        q = w.keys[:ns].cpu().numpy()
+        fid = w.fid[:ns].cpu().numpy().view(np.uint32)
+        bms = w.bitmaps.cpu().numpy()
+        off = w.bitmap_off_host
+        sl = [slice(i, min(ns, i + (ns + cores - 1) // cores)) for i in range(0, ns, (ns + cores - 1) // cores)]
+        with ThreadPoolExecutor(cores) as ex:
+            def run():
+                list(ex.map(lambda s_: O.probe_multi(q[s_], fid[s_], bms, off, bits_per_key=BPK), sl))
+            reps, t = _timed_reps(run, budget_s)
+        return {"value": round(ns * reps / t / 1e6, 3), "unit": "Mqueries/s", "cores": cores, "kind": "port",
+                "sample": f"{reps} x the first {ns // 1000}k queries of this GPU's batch, query slices on "
+                          f"{cores} threads, oracle_probe_multi (C restatement of src/filter_block.cpp:49-62), "
+                          f"{t:.1f} s"}
+    n = 10_000_000
+    keys = O.splitmix_keys16(0x5EED, n)
+    reps, t_total = _timed_reps(lambda: O.keys2block(keys, bits_per_key=BPK), budget_s)
     return {"value": round(n * reps / t_total / 1e6, 3), "unit": "Mkeys/s", "cores": 1, "kind": "port",
             "sample": f"{reps} x full 10M x 16B-key build (seed 0x5EED, bpk=10), oracle_keys2block "
                       f"(C restatement of src/filter_block.cpp:9-33, gcc -O2), {t_total:.1f} s"}
+
+
+def probe_check(w, out):
+    """Probe results: every inserted-key query must hit (full batch, on the
+    device); the false-positive rate over fresh keys; and a 200k-query sample
+    plus two tables' bitmaps compared bit for bit with the oracle."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import numpy as np
+
+    import oracle as O
+
+    mem = w.member.bool()
+    hits_ins = int(out[mem].sum().item())
+    n_ins = int(mem.sum().item())
+    fp = int(out[~mem].sum().item())
+    n_fresh = w.n - n_ins
+    ns = min(w.n, 200_000)
+    bms = w.bitmaps.cpu().numpy()
+    off = w.bitmap_off_host
+    want = O.probe_multi(w.keys[:ns].cpu().numpy(), w.fid[:ns].cpu().numpy().view(np.uint32), bms, off,
+                         bits_per_key=BPK)
+    sample_ok = bool(np.array_equal(out[:ns].cpu().numpy(), want))
+    tab_ok = True
+    for li in (0, len(w.tables) - 1):
+        t = w.tables[li]
+        ref = O.keys2block(O.splitmix_keys16(0x5EED + t, PROBE_KEYS_PER_TABLE), bits_per_key=BPK)
+        tab_ok &= bool(np.array_equal(bms[int(off[li]):int(off[li + 1])], ref))
+    return {"hit_rate_inserted": round(hits_ins / max(n_ins, 1), 6), "false_negatives": n_ins - hits_ins,
+            "fpr_fresh": round(fp / max(n_fresh, 1), 6), "queries_inserted": n_ins, "queries_fresh": n_fresh,
+            "oracle_sample": f"{ns} queries {'bit-identical' if sample_ok else 'MISMATCH'} vs oracle_probe_multi",
+            "oracle_bitmaps": "tables %d,%d %s" % (w.tables[0], w.tables[-1],
+                                                   "bit-identical" if tab_ok else "MISMATCH")}
+
+
+def hbm_stream_read_gbs(nbytes=4 << 30, reps=5):
+    """Measured streaming-read bandwidth of this GPU (lib/libadlhbm.so, nontemporal
+    16 B loads, persistent grid), best of `reps` over a buffer 16x the Infinity Cache."""
+    import ctypes
+
+    import torch
+
+    path = os.path.join(ROOT, "adlsm-tree_amd", "lib", "libadlhbm.so")
+    L = ctypes.CDLL(path)
+    L.adl_hbm_stream_read.restype = ctypes.c_int
+    L.adl_hbm_stream_read.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint32,
+                                      ctypes.c_void_p]
+    buf = torch.ones(nbytes // 8, dtype=torch.int64, device="cuda")
+    sink = torch.zeros(1 << 16, dtype=torch.int32, device="cuda")
+    st = torch.cuda.current_stream()
+    best = 0.0
+    for _ in range(reps + 1):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        rc = L.adl_hbm_stream_read(buf.data_ptr(), nbytes, sink.data_ptr(), sink.numel(),
+                                   ctypes.c_void_p(st.cuda_stream))
+        e1.record(st)
+        e1.synchronize()
+        if rc:
+            return None
+        best = max(best, nbytes / (e0.elapsed_time(e1) * 1e-3) / 1e9)
+    del buf
+    return round(best, 1)
 
 
 def e2e(n, iters=5):
@@ -196,42 +375,70 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
-    w = Workload(args.workload, rank, args.keys, world)
+    w = Workload(args.workload, rank, args.keys, world, args.queries)
+    probe = args.workload == "probe"
     torch.cuda.synchronize()
     for _ in range(args.warmup):
         w.step()
     barrier()
     ab.profile_enable(max(args.steps, 1) * 64)  # launch pairs: a segmented build runs one per 8 filters
+    # probe: one kernel per step on torch's current stream, bracketed by events there
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(args.steps)] if probe else []
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        bm = w.step()
+    for i in range(args.steps):
+        if probe:
+            ev[i][0].record()
+        out = w.step()
+        if probe:
+            ev[i][1].record()
     barrier()
     elapsed = time.perf_counter() - t0
     ms_a, ms_b, nb = ab.profile_collect()
+    probe_ms = sum(a.elapsed_time(b) for a, b in ev) / max(args.steps, 1) if probe else 0.0
 
     # RCCL: the only collective -- sum of keys built, max of elapsed time
     from adlbloom import dist as D
 
     total_keys, elapsed_max = D.reduce_throughput(float(w.n) * args.steps, elapsed, device="cuda")
 
-    parity = parity_check(bm, w.n) if (rank == 0 and args.workload == "single") else None
+    parity = None
+    if rank == 0 and args.workload == "single":
+        parity = parity_check(out, w.n)
+    elif rank == 0 and probe:
+        parity = probe_check(w, out)
 
     if rank == 0:
-        # kernel time per step (a segmented build is one launch pair per group of 8 filters)
-        kern_ms = (ms_a + ms_b) / max(args.steps, 1)
-        achieved = w.bytes_per_launch / (kern_ms * 1e-3) / 1e9 if nb else None
+        if probe:
+            kern_ms = probe_ms
+            kernels = {"bloom_probe_multi_kernel": round(probe_ms * 1e3, 2)}
+            kname = "bloom_probe_multi_kernel"
+        else:
+            # kernel time per step (a segmented build is one launch pair per group of 8 filters)
+            kern_ms = (ms_a + ms_b) / max(args.steps, 1)
+            kernels = {"bloom_bin_kernel": round(ms_a / max(args.steps, 1) * 1e3, 2),
+                       "bloom_tile_kernel": round(ms_b / max(args.steps, 1) * 1e3, 2)}
+            kname = "bloom_bin_kernel + bloom_tile_kernel (one build = the pair)"
+        timed = kern_ms > 0 and (probe or nb)
+        achieved = w.bytes_per_launch / (kern_ms * 1e-3) / 1e9 if timed else None
         traffic = load_traffic(args.workload, w.bytes_per_launch)
-        out = {
-            "metric": "Mkeys/s bloom-filter build (device-resident), 16B keys, bits/key=10"
-            if args.workload != "varlen" else "Mkeys/s bloom-filter build (device-resident), var-len keys, bits/key=10",
+        stream_gbs = hbm_stream_read_gbs()
+        if probe:
+            metric = "Mqueries/s bloom-filter probe (device-resident), 16B keys, 256 filters, bits/key=10"
+        elif args.workload == "varlen":
+            metric = "Mkeys/s bloom-filter build (device-resident), var-len keys, bits/key=10"
+        else:
+            metric = "Mkeys/s bloom-filter build (device-resident), 16B keys, bits/key=10"
+        out_json = {
+            "metric": metric,
             "value": round(total_keys / elapsed_max / 1e6, 1),
-            "unit": "Mkeys/s",
+            "unit": "Mqueries/s" if probe else "Mkeys/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed_max / max(args.steps, 1) * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if probe else "weak",
             "vs_baseline": None,
             "dtype": w.dtype,
             "data": "synthetic (SplitMix64 keys generated on device, SURVEY.md §8d)",
@@ -243,23 +450,24 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
                 "traffic": traffic,
-                "kernel": "bloom_bin_kernel + bloom_tile_kernel (one build = the pair)",
-                "algorithmic_bytes_per_build": w.bytes_per_launch,
-                "us_per_build": {"bloom_bin_kernel": round(ms_a / max(args.steps, 1) * 1e3, 2),
-                                 "bloom_tile_kernel": round(ms_b / max(args.steps, 1) * 1e3, 2)},
-                "launch_pairs_per_build": round(nb / max(args.steps, 1), 2),
+                "kernel": kname,
+                "algorithmic_bytes_per_step": w.bytes_per_launch,
+                "us_per_step": kernels,
+                "launch_pairs_per_build": None if probe else round(nb / max(args.steps, 1), 2),
                 "read_only_frac": round(16 * w.n / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
-                if (nb and args.workload != "varlen") else None,
+                if (timed and args.workload in ("single", "compaction")) else None,
+                "measured_stream_read_gbs": stream_gbs,
+                "frac_of_measured_stream_read": round(achieved / stream_gbs, 4) if (achieved and stream_gbs) else None,
             },
             "parity": parity,
         }
         if world == 1 and args.workload == "single" and not args.no_e2e:
-            out["e2e"] = e2e(w.n)
+            out_json["e2e"] = e2e(w.n)
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+            out_json["cpu_baseline"] = cpu_baseline(args.cpu_seconds, args.workload, w)
         else:
-            out["cpu_baseline"] = None
-        print(json.dumps(out), flush=True)
+            out_json["cpu_baseline"] = None
+        print(json.dumps(out_json), flush=True)
     if world > 1:
         dist.destroy_process_group()
 

@@ -196,6 +196,16 @@ int adl_synth_varlen_lengths_device(uint32_t *d_lengths, uint64_t seed, uint64_t
                                     void *stream);
 int adl_synth_varlen_fill_device(uint8_t *d_out, uint64_t seed, uint64_t total_bytes, void *stream);
 
+/* Probe queries of BASELINE.json configs[4] (DESIGN.md "Synthetic inputs"):
+ * global query q = q0 + i draws four SplitMix64 outputs of the stream seeded
+ * `seed` (calls 4q+1 .. 4q+4): r0 -> filter id r0 % num_tables; r1 odd -> an
+ * inserted key, key j = (r1 >> 1) % keys_per_table of table t's key stream
+ * (adl_synth_keys16_device(seed = table_seed0 + t)); r1 even -> a fresh key
+ * LE64(r2) || LE64(r3).  d_member[i] = 1 for inserted keys (may be NULL). */
+int adl_synth_probe_queries_device(uint8_t *d_keys, uint32_t *d_filter_id, uint8_t *d_member,
+                                   uint64_t seed, uint64_t q0, uint64_t n, uint32_t num_tables,
+                                   uint64_t table_seed0, uint64_t keys_per_table, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

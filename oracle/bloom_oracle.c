@@ -210,3 +210,38 @@ void oracle_splitmix_keys16(uint64_t seed, uint64_t skip, uint64_t n, uint8_t *o
     memcpy(out + 8 * i, &z, 8); /* little-endian host */
   }
 }
+
+/* SplitMix64 output number `call` (1-based) of the stream seeded `seed`. */
+static uint64_t oracle_splitmix_at(uint64_t seed, uint64_t call) {
+  uint64_t z = seed + call * 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+/* Probe queries of BASELINE.json configs[4] (probe config):
+ * query q draws outputs 4q+1..4q+4 of the stream seeded `seed`: r0 picks the
+ * filter (r0 % num_tables), r1 odd picks inserted key (r1>>1) % keys_per_table
+ * of that table's oracle_splitmix_keys16(table_seed0 + t) stream, r1 even a
+ * fresh key LE64(r2) || LE64(r3).  member[q] = 1 for inserted keys. */
+void oracle_synth_probe_queries(uint64_t seed, uint64_t q0, uint64_t n, uint32_t num_tables,
+                                uint64_t table_seed0, uint64_t keys_per_table, uint8_t *keys,
+                                uint32_t *filter_id, uint8_t *member) {
+  for (uint64_t i = 0; i < n; i++) {
+    uint64_t c = 4 * (q0 + i);
+    uint64_t r0 = oracle_splitmix_at(seed, c + 1), r1 = oracle_splitmix_at(seed, c + 2);
+    uint32_t t = (uint32_t)(r0 % num_tables);
+    int ins = (r1 & 1) && keys_per_table;
+    uint64_t kv[2];
+    if (ins) {
+      uint64_t j = (r1 >> 1) % keys_per_table;
+      oracle_splitmix_keys16(table_seed0 + t, j, 1, keys + 16 * i);
+    } else {
+      kv[0] = oracle_splitmix_at(seed, c + 3);
+      kv[1] = oracle_splitmix_at(seed, c + 4);
+      memcpy(keys + 16 * i, kv, 16);
+    }
+    filter_id[i] = t;
+    if (member) member[i] = (uint8_t)ins;
+  }
+}

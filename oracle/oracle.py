@@ -63,6 +63,10 @@ def lib():
                                            ctypes.c_uint32, ctypes.c_uint32, u8p]
         L.oracle_splitmix_keys16.restype = None
         L.oracle_splitmix_keys16.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, u8p]
+        L.oracle_synth_probe_queries.restype = None
+        L.oracle_synth_probe_queries.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
+                                                 ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64,
+                                                 u8p, u8p, u8p]
         _LIB = L
     return _LIB
 
@@ -95,6 +99,17 @@ def splitmix_keys16(seed: int, n: int, skip: int = 0) -> np.ndarray:
     out = np.empty((n, 16), dtype=np.uint8)
     lib().oracle_splitmix_keys16(seed, skip, n, _ptr(out))
     return out
+
+
+def synth_probe_queries(n: int, seed: int = 0xFEED, q0: int = 0, num_tables: int = 256,
+                        table_seed0: int = 0x5EED, keys_per_table: int = 1_000_000):
+    """Probe queries of BASELINE.json configs[4]: (keys (n,16) u8, filter_id u32, member u8)."""
+    keys = np.empty((n, 16), dtype=np.uint8)
+    fid = np.empty(n, dtype=np.uint32)
+    member = np.empty(n, dtype=np.uint8)
+    lib().oracle_synth_probe_queries(seed, q0, n, num_tables, table_seed0, keys_per_table,
+                                     _ptr(keys), _ptr(fid), _ptr(member))
+    return keys, fid, member
 
 
 def pack(keys) -> tuple[np.ndarray, np.ndarray]:

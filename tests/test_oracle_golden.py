@@ -165,3 +165,17 @@ def test_var_len_and_duplicates(oracle):
     data, offs = oracle.pack(keys)
     assert np.array_equal(oracle.keys2block(data, offs), bm)
     assert bm.size == n * 10 + 7
+
+
+def test_oracle_probe_queries_generator(oracle):
+    """configs[4] query generator: filter ids cover the tables, half the queries are
+    inserted keys and each of those is key j of its table's SplitMix64 stream."""
+    import numpy as np
+
+    k, f, m = oracle.synth_probe_queries(3000, num_tables=5, keys_per_table=40)
+    assert set(np.unique(f)) == set(range(5))
+    assert 0.4 < m.mean() < 0.6
+    for i in np.nonzero(m)[0][:50]:
+        assert (oracle.splitmix_keys16(0x5EED + int(f[i]), 40) == k[i]).all(1).any()
+    k2, f2, m2 = oracle.synth_probe_queries(1000, q0=2000, num_tables=5, keys_per_table=40)
+    assert np.array_equal(k2, k[2000:]) and np.array_equal(f2, f[2000:]) and np.array_equal(m2, m[2000:])

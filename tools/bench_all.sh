@@ -3,12 +3,12 @@
 set -u
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
-for wl in ${WORKLOADS:-single varlen compaction}; do
+for wl in ${WORKLOADS:-single varlen compaction probe}; do
   timeout -k 10 600 python3 bench.py --steps ${STEPS:-20} --warmup 3 --workload $wl --no-cpu-baseline --no-e2e \
     > gpurun_out/bench_$wl.log 2>&1
   rc=$?
   echo "=== $wl rc=$rc"
-  grep '^{' gpurun_out/bench_$wl.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["unit"], d["ms_per_step"], "ms", d["roofline"]["us_per_build"], d["roofline"]["frac"], d["parity"])' || tail -5 gpurun_out/bench_$wl.log
+  grep '^{' gpurun_out/bench_$wl.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["unit"], d["ms_per_step"], "ms", d["roofline"]["us_per_step"], d["roofline"]["frac"], d["parity"])' || tail -5 gpurun_out/bench_$wl.log
   [ $rc -ne 0 ] && exit $rc
 done
 exit 0
