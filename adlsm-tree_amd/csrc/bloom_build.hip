@@ -430,21 +430,24 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin16_kernel(BuildArgs a, Keys16 
   const uint32_t slot =
       (a.xcd_remap && G % 8 == 0) ? (blockIdx.x % 8) * (G / 8) + blockIdx.x / 8 : blockIdx.x;
 
-  auto chunk_cnt = [&](uint32_t chunk) -> uint32_t {
-    const FilterDesc &d = a.f[find_filter_by_chunk(a, chunk)];
-    return min(C, d.n - (chunk - d.chunk_base) * C);
-  };
+  // Every global load and store of the chunk loop below is issued
+  // unconditionally (out-of-range lanes load a clamped key, and store to
+  // their wave's scratch line), so the compiler can count them: the hash of
+  // chunk c+1 waits only for its own keys (vmcnt(stores issued since)), not
+  // for every outstanding store of chunk c-1 and the table (vmcnt(0)).
+  const int wave = tid / kWave;
+  uint32_t *dummy = tile_queue + 64 + ((uint64_t)blockIdx.x * (BLOCK / kWave) + wave) * 4;
+  uint4 *dummy4 = reinterpret_cast<uint4 *>(dummy);
+  constexpr int TPT = (int)((kHistMax + BLOCK - 1) / BLOCK);  // table entries per thread, at most
+
   auto fetch = [&](uint32_t chunk, uint4 (&raw)[KPT]) {
     const FilterDesc &d = a.f[find_filter_by_chunk(a, chunk)];
     const uint32_t first = (chunk - d.chunk_base) * C;
-    const uint32_t cnt = min(C, d.n - first);
+    const uint32_t last = min(C, d.n - first) - 1u;
 #pragma unroll
     for (int i = 0; i < KPT; ++i) {
-      const uint32_t idx = tid + i * BLOCK;
-      if (idx < cnt) {
-        const uint4 *src = keys.keys + d.key_begin + first + idx;
-        raw[i] = a.nt_keys ? load_nt(src) : *src;
-      }
+      const uint32_t idx = min((uint32_t)(tid + i * BLOCK), last);
+      raw[i] = load_nt(keys.keys + d.key_begin + first + idx);
     }
   };
 
@@ -453,15 +456,13 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin16_kernel(BuildArgs a, Keys16 
   if (slot >= total_chunks) return;
   {
     fetch(slot, raw);
-    const uint32_t cnt0 = chunk_cnt(slot);
 #pragma unroll
-    for (int i = 0; i < KPT; ++i)
-      if (tid + i * BLOCK < cnt0) hash16(raw[i], h1[i], h2[i]);
-    if (slot + G < total_chunks) fetch(slot + G, raw);
+    for (int i = 0; i < KPT; ++i) hash16(raw[i], h1[i], h2[i]);
+    fetch(min(slot + G, total_chunks - 1), raw);
   }
   for (uint32_t i = tid; i < a.hist_words; i += BLOCK) hist[i] = 0;
 
-  uint4 *pdst = nullptr;  // deferred store of the previous chunk
+  uint4 *pdst = dummy4;  // deferred store of the previous chunk
   uint32_t ptotal = 0;
   for (uint32_t wg = slot; wg < total_chunks; wg += G) {
     const FilterDesc &d = a.f[find_filter_by_chunk(a, wg)];
@@ -489,21 +490,28 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin16_kernel(BuildArgs a, Keys16 
 #pragma unroll
       for (int sv = i * SPI; sv < (i + 1) * SPI && sv < VPT; ++sv) {
         const uint32_t v = tid + sv * BLOCK;
-        if (v < pvec) pdst[v] = src4[v];
+        const bool ok = v < pvec;
+        *(ok ? pdst + v : dummy4) = src4[ok ? v : 0u];
       }
     }
-    if ((uint32_t)tid < (ptotal & 3u))
-      reinterpret_cast<uint32_t *>(pdst)[pvec * 4 + tid] = lpos[pvec * 4 + tid];
+    {
+      const bool ok = (uint32_t)tid < (ptotal & 3u);
+      *(ok ? reinterpret_cast<uint32_t *>(pdst) + pvec * 4 + tid : dummy) = lpos[ok ? pvec * 4 + tid : 0u];
+    }
     __syncthreads();  // counts complete; the previous chunk's LDS copy is read out
 
     block_excl_scan_array<BLOCK>(hist, T + 1, scratch);
     uint32_t *tab = table_ws + d.table_base;
-    for (uint32_t t = tid; t <= T; t += BLOCK) tab[(uint64_t)t * d.chunks + w] = hist[t];
+#pragma unroll
+    for (int r = 0; r < TPT; ++r) {
+      const uint32_t t = tid + r * BLOCK;
+      const bool ok = t <= T;
+      *(ok ? tab + (uint64_t)t * d.chunks + w : dummy) = hist[ok ? t : 0u];
+    }
     __syncthreads();
 
-    // scatter(c) + hash(c+1) (its keys arrived during the previous chunk)
-    const bool has_next = wg + G < total_chunks;
-    const uint32_t cnt_n = has_next ? chunk_cnt(wg + G) : 0u;
+    // scatter(c) + hash(c+1) (its keys arrived during the previous chunk;
+    // lanes past the end hash a clamped key and never use the result)
 #pragma unroll
     for (int i = 0; i < KPT; ++i) {
       if (tid + i * BLOCK < cnt) {
@@ -513,9 +521,9 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin16_kernel(BuildArgs a, Keys16 
 #pragma unroll
         for (int j = 0; j < K; ++j) lpos[sl[j]] = pos[i][j] & tmask;
       }
-      if (tid + i * BLOCK < cnt_n) hash16(raw[i], h1[i], h2[i]);
+      hash16(raw[i], h1[i], h2[i]);
     }
-    if (wg + 2 * G < total_chunks) fetch(wg + 2 * G, raw);
+    fetch(min(wg + 2 * G, total_chunks - 1), raw);
     __syncthreads();  // lpos holds chunk c sorted; hist is free
     for (uint32_t i = tid; i <= T; i += BLOCK) hist[i] = 0;
     pdst = reinterpret_cast<uint4 *>(pos_ws + d.pos_base + (uint64_t)w * a.cap);
@@ -636,13 +644,24 @@ __global__ __launch_bounds__(kBlockB) void bloom_tile_kernel(BuildArgs a,
         if (lane < D && q < Q) dsc = seg[wave + NWAVES * q];
         st.base = dsc.x;
         st.len = dsc.y;
+        // The segment base is wave-uniform: an SGPR pointer plus the lane's
+        // constant byte offset, so a gather needs no per-slot address VALU.
+        // Positions 0-63 are loaded by every lane, unconditionally (lanes past
+        // the segment read the next segment's words, inside the workspace's
+        // slack, and are masked in consume): with no branch around them the
+        // compiler can wait for one stage's loads (vmcnt(D)) instead of all.
+        uint32_t len[D];
+        const uint32_t *sp[D];
 #pragma unroll
         for (int u = 0; u < D; ++u) {
-          const uint32_t len = __builtin_amdgcn_readlane(st.len, u);
-          const uint32_t b = __builtin_amdgcn_readlane(st.base, u);
-          if ((uint32_t)lane < len) st.v0[u] = pos_ws[b + lane];
-          if (len > (uint32_t)kWave && (uint32_t)lane + kWave < len) st.v1[u] = pos_ws[b + kWave + lane];
+          len[u] = __builtin_amdgcn_readlane(st.len, u);
+          sp[u] = pos_ws + __builtin_amdgcn_readlane(st.base, u);
         }
+#pragma unroll
+        for (int u = 0; u < D; ++u)
+          if (len[u] > (uint32_t)kWave && (uint32_t)lane + kWave < len[u]) st.v1[u] = sp[u][kWave + lane];
+#pragma unroll
+        for (int u = 0; u < D; ++u) st.v0[u] = sp[u][lane];
       };
       auto consume = [&](const Stage &st) {
 #pragma unroll
@@ -727,7 +746,7 @@ inline KeysVar shift_keys(KeysVar k, uint64_t b) { k.offs += b; return k; }
 // ---------------------------------------------------------------- host plan
 struct Plan {
   BuildArgs a;
-  uint64_t pos_words = 0, table_words = 0, ws_bytes = 0;
+  uint64_t pos_words = 0, table_words = 0, scratch_words = 0, ws_bytes = 0;
   uint32_t total_chunks = 0, total_tiles = 0;
   uint32_t grid_a = 0, grid_b = 0;  // persistent grids
   uint32_t block_a = 512;             // pass A threads per workgroup
@@ -846,7 +865,10 @@ int make_plan(const uint64_t *counts, uint32_t nf, int32_t bpk, Plan &p) {
   p.total_tiles = tile;
   p.pos_words = adl_host::round_up(pos, 64);
   p.table_words = adl_host::round_up(tab + kTablePad, 64);
-  p.ws_bytes = (p.pos_words + p.table_words) * 4 + 256;
+  // after the table: pass B's tile queue (64 words), then one 16-byte scratch
+  // line per pass-A wave (bloom_bin16_kernel's masked-off stores)
+  p.scratch_words = 64 + (uint64_t)grid_a_max * (block_a / kWave) * 4;
+  p.ws_bytes = (p.pos_words + p.table_words + p.scratch_words) * 4 + 256;
   p.lds_a = (size_t)(hist_words + 32 + (k + 1) * C + 256) * 4;
   p.lds_b = (size_t)((1u << (TL - 5)) + 2 * kSegBatch + 4) * 4;
   p.grid_a = std::min<uint32_t>(p.total_chunks, grid_a_max);
@@ -885,7 +907,7 @@ template <class Keys>
 int launch_binned(const Plan &p, Keys keys, uint8_t *d_bitmaps, void *ws, hipStream_t st) {
   uint32_t *pos_ws = reinterpret_cast<uint32_t *>(ws);
   uint32_t *tab_ws = pos_ws + p.pos_words;
-  uint32_t *queue = tab_ws + p.table_words;  // pass B tile queue (inside the +256 B slack)
+  uint32_t *queue = tab_ws + p.table_words;  // pass B tile queue, then pass A's scratch lines
   hipEvent_t *ev = prof_slot();
   if (ev) ADL_HIP_TRY(hipEventRecord(ev[0], st));
   if (p.total_chunks) {

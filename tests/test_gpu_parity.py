@@ -319,9 +319,12 @@ def test_probe_multi_many_filters(dev, ab, oracle, F):
     assert np.array_equal(got, oracle.probe_multi(q, fid, flat, boff))
 
 
+@pytest.mark.parametrize("groups", [None, "2,4", "8,8", "1,3"])
 @pytest.mark.parametrize("bpk", [1, 3, 10, 40])
-def test_probe_read_grouping_all_k(dev, ab, oracle, bpk):
-    """k = 1, 2, 6, 27: the bitmap reads are issued 2 then 4 at a time."""
+def test_probe_read_grouping_all_k(dev, ab, oracle, bpk, groups, monkeypatch):
+    """k = 1, 2, 6, 27 under several read groupings (ADL_BLOOM_PROBE_GROUPS)."""
+    if groups:
+        monkeypatch.setenv("ADL_BLOOM_PROBE_GROUPS", groups)
     keys = oracle.splitmix_keys16(0xABC, 20000)
     bm = oracle.keys2block(keys, bits_per_key=bpk)
     q = np.concatenate([keys[:5000], oracle.splitmix_keys16(0xABD, 30000)])
