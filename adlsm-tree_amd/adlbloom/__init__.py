@@ -18,7 +18,9 @@ import os
 import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_DIR, "lib", "libadlbloom.so")
+# ADL_BLOOM_LIB: diagnostics only (tools/stamps.py points it at the
+# s_memtime-instrumented build, lib_stamps/libadlbloom.so)
+LIB_PATH = os.environ.get("ADL_BLOOM_LIB") or os.path.join(PKG_DIR, "lib", "libadlbloom.so")
 
 SEED1 = 0xE2C6928A  # src/filter_block.cpp:22
 SEED2 = 0xBAEA8A8F  # src/filter_block.cpp:23

@@ -63,8 +63,7 @@ struct FilterDesc {
   uint32_t chunks;      // W
   uint32_t tiles;       // T
   FastMod mod;          // m = 8 * bitmap bytes
-  uint32_t wrap;        // 2^32 mod m (incremental positions)
-  uint32_t pad_;
+  uint32_t pad_[2];
 };
 
 struct BuildArgs {
@@ -78,8 +77,8 @@ struct BuildArgs {
   uint32_t nt_keys;    // pass A: non-temporal key loads (tuning, ADL_BLOOM_NT_KEYS)
   uint32_t nt_bitmap;  // pass B: non-temporal bitmap stores (tuning, ADL_BLOOM_NT_BITMAP)
   uint32_t dyn_tiles;  // pass B: tiles from a work queue that pass A resets (ADL_BLOOM_DYN_TILES)
-  uint32_t inc_pos;    // pass A: incremental positions (ADL_BLOOM_INC_POS)
   uint32_t stage_keys; // pass A: LDS-staged variable-length keys (16-B aligned key buffer; ADL_BLOOM_STAGE_KEYS)
+  uint32_t exp;        // diagnostics build only (ADL_BLOOM_EXP bits, wrong results): 1 no hash, 2 no stores
   FilterDesc f[kMaxFilters];
 };
 
@@ -98,6 +97,33 @@ __device__ __forceinline__ int find_filter_by_tile(const BuildArgs &a, uint32_t 
     if ((uint32_t)i < a.nf && wg >= a.f[i].tile_base) f = i;
   return f;
 }
+
+// ---------------------------------------------------------------- diagnostics
+// Built only with -DADL_BLOOM_STAMPS (make stamps): wave 0 of every
+// workgroup accumulates s_memtime cycles per kernel phase; read back with
+// adl_bloom_debug_stamps() (tools/stamps.py).  The product library has none
+// of this.
+#ifdef ADL_BLOOM_STAMPS
+__device__ uint64_t g_stamps[2][2048][8];
+#define STAMP_DECL                                  \
+  uint64_t st_acc_[8] = {0, 0, 0, 0, 0, 0, 0, 0}; \
+  uint64_t st_t_ = __builtin_amdgcn_s_memtime();
+#define STAMP(i)                                      \
+  do {                                                \
+    const uint64_t t_ = __builtin_amdgcn_s_memtime(); \
+    st_acc_[i] += t_ - st_t_;                         \
+    st_t_ = t_;                                       \
+  } while (0)
+#define STAMP_FLUSH(pass)                                                         \
+  do {                                                                            \
+    if (threadIdx.x == 0 && blockIdx.x < 2048)                                    \
+      for (int i_ = 0; i_ < 8; ++i_) g_stamps[pass][blockIdx.x][i_] = st_acc_[i_]; \
+  } while (0)
+#else
+#define STAMP_DECL
+#define STAMP(i) do { } while (0)
+#define STAMP_FLUSH(pass) do { } while (0)
+#endif
 
 // ---------------------------------------------------------------- pass A
 // Register prefetch of a chunk's keys.  Only the fixed 16-byte view has raw
@@ -383,30 +409,6 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin_kernel(BuildArgs a, Keys keys
 //   prefetch keys of c+2
 // so the murmur work hides under the scatter's LDS latency and the position
 // stores drain under the next count.
-// The k positions (h1 + j*h2) % m of one key, j = 0..K-1, from two
-// reductions instead of K: with d = h2 % m and W = 2^32 % m,
-//   p_{j+1} = (p_j + d - c_j * W) mod m,
-// where c_j is the carry out of the 32-bit add h_j + h2 (h_{j+1} wraps by 2^32).
-template <int K>
-__device__ __forceinline__ void positions_inc(uint32_t h1, uint32_t h2, const FastMod &mod, uint32_t wrap,
-                                              uint32_t (&pos)[K]) {
-  const uint32_t m = mod.m;
-  const uint32_t d = fastmod(h2, mod);
-  uint32_t p = fastmod(h1, mod), h = h1;
-#pragma unroll
-  for (int j = 0; j < K; ++j) {
-    pos[j] = p;
-    if (j + 1 < K) {
-      const uint32_t hn = h + h2;
-      uint32_t t = p + d;
-      t = t >= m ? t - m : t;
-      if (hn < h) t = t >= wrap ? t - wrap : t + (m - wrap);
-      p = t;
-      h = hn;
-    }
-  }
-}
-
 template <int BLOCK, int K>
 __global__ __launch_bounds__(BLOCK) void bloom_bin16_kernel(BuildArgs a, Keys16 keys,
                                                               uint32_t *__restrict__ pos_ws,
@@ -451,19 +453,21 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin16_kernel(BuildArgs a, Keys16 
     }
   };
 
+  // The keys of chunk c+2 load at the end of step c (two chunks ahead) and
+  // are hashed in step c+1.  Measured against loading chunk c+1's keys at the
+  // top of step c (no load in flight across the back-edge): 111 vs 127 us.
   uint4 raw[KPT];
   uint32_t h1[KPT], h2[KPT];
   if (slot >= total_chunks) return;
-  {
-    fetch(slot, raw);
+  fetch(slot, raw);
 #pragma unroll
-    for (int i = 0; i < KPT; ++i) hash16(raw[i], h1[i], h2[i]);
-    fetch(min(slot + G, total_chunks - 1), raw);
-  }
+  for (int i = 0; i < KPT; ++i) hash16(raw[i], h1[i], h2[i]);
+  fetch(min(slot + G, total_chunks - 1), raw);
   for (uint32_t i = tid; i < a.hist_words; i += BLOCK) hist[i] = 0;
 
   uint4 *pdst = dummy4;  // deferred store of the previous chunk
   uint32_t ptotal = 0;
+  STAMP_DECL
   for (uint32_t wg = slot; wg < total_chunks; wg += G) {
     const FilterDesc &d = a.f[find_filter_by_chunk(a, wg)];
     const uint32_t w = wg - d.chunk_base;
@@ -471,6 +475,7 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin16_kernel(BuildArgs a, Keys16 
     const uint32_t T = d.tiles;
     const FastMod mod = d.mod;
     __syncthreads();  // hist cleared; the previous scatter is complete in lpos
+    STAMP(0);
 
     // count(c) + store(c-1)
     const uint32_t pvec = ptotal >> 2;
@@ -478,19 +483,18 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin16_kernel(BuildArgs a, Keys16 
 #pragma unroll
     for (int i = 0; i < KPT; ++i) {
       if (tid + i * BLOCK < cnt) {
-        if (a.inc_pos) {
-          positions_inc<K>(h1[i], h2[i], mod, d.wrap, pos[i]);
-        } else {
 #pragma unroll
-          for (int j = 0; j < K; ++j) pos[i][j] = fastmod(h1[i] + (uint32_t)j * h2[i], mod);
-        }
+        for (int j = 0; j < K; ++j) pos[i][j] = fastmod(h1[i] + (uint32_t)j * h2[i], mod);
 #pragma unroll
         for (int j = 0; j < K; ++j) atomicAdd(&hist[pos[i][j] >> TL], 1u);
       }
 #pragma unroll
       for (int sv = i * SPI; sv < (i + 1) * SPI && sv < VPT; ++sv) {
         const uint32_t v = tid + sv * BLOCK;
-        const bool ok = v < pvec;
+        bool ok = v < pvec;
+#ifdef ADL_BLOOM_STAMPS
+        if (a.exp & 2) ok = false;
+#endif
         *(ok ? pdst + v : dummy4) = src4[ok ? v : 0u];
       }
     }
@@ -499,8 +503,10 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin16_kernel(BuildArgs a, Keys16 
       *(ok ? reinterpret_cast<uint32_t *>(pdst) + pvec * 4 + tid : dummy) = lpos[ok ? pvec * 4 + tid : 0u];
     }
     __syncthreads();  // counts complete; the previous chunk's LDS copy is read out
+    STAMP(1);
 
     block_excl_scan_array<BLOCK>(hist, T + 1, scratch);
+    STAMP(2);
     uint32_t *tab = table_ws + d.table_base;
 #pragma unroll
     for (int r = 0; r < TPT; ++r) {
@@ -509,6 +515,7 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin16_kernel(BuildArgs a, Keys16 
       *(ok ? tab + (uint64_t)t * d.chunks + w : dummy) = hist[ok ? t : 0u];
     }
     __syncthreads();
+    STAMP(3);
 
     // scatter(c) + hash(c+1) (its keys arrived during the previous chunk;
     // lanes past the end hash a clamped key and never use the result)
@@ -521,10 +528,17 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin16_kernel(BuildArgs a, Keys16 
 #pragma unroll
         for (int j = 0; j < K; ++j) lpos[sl[j]] = pos[i][j] & tmask;
       }
+#ifdef ADL_BLOOM_STAMPS
+      if (a.exp & 1) {
+        h1[i] = raw[i].x;
+        h2[i] = raw[i].y | 1u;
+      } else
+#endif
       hash16(raw[i], h1[i], h2[i]);
     }
     fetch(min(wg + 2 * G, total_chunks - 1), raw);
     __syncthreads();  // lpos holds chunk c sorted; hist is free
+    STAMP(4);
     for (uint32_t i = tid; i <= T; i += BLOCK) hist[i] = 0;
     pdst = reinterpret_cast<uint4 *>(pos_ws + d.pos_base + (uint64_t)w * a.cap);
     ptotal = K * cnt;
@@ -534,6 +548,8 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin16_kernel(BuildArgs a, Keys16 
   for (uint32_t v = tid; v < pvec; v += BLOCK) pdst[v] = src4[v];
   if ((uint32_t)tid < (ptotal & 3u))
     reinterpret_cast<uint32_t *>(pdst)[pvec * 4 + tid] = lpos[pvec * 4 + tid];
+  STAMP(5);
+  STAMP_FLUSH(0);
 }
 
 // ---------------------------------------------------------------- pass B
@@ -601,6 +617,11 @@ __global__ __launch_bounds__(kBlockB) void bloom_tile_kernel(BuildArgs a,
   }
   uint32_t pre_s[RPT], pre_e[RPT];
   if (wg < total_tiles) fetch_rows(wg, 0, pre_s, pre_e);
+  {  // the tile starts zeroed; every write-out re-zeroes it
+    uint4 *t4w = reinterpret_cast<uint4 *>(tile);
+    for (uint32_t i = tid; i < tile_words / 4; i += kBlockB) t4w[i] = make_uint4(0, 0, 0, 0);
+  }
+  STAMP_DECL
 
   while (wg < total_tiles) {
     const FilterDesc &d = a.f[find_filter_by_tile(a, wg)];
@@ -609,9 +630,8 @@ __global__ __launch_bounds__(kBlockB) void bloom_tile_kernel(BuildArgs a,
     const uint32_t pos_base = (uint32_t)d.pos_base;
 
     if (a.dyn_tiles && tid == 0) qs[1] = atomicAdd(tile_queue, 1u);
-    uint4 *t4w = reinterpret_cast<uint4 *>(tile);
-    for (uint32_t i = tid; i < tile_words / 4; i += kBlockB) t4w[i] = make_uint4(0, 0, 0, 0);
-    __syncthreads();  // tile zeroed (also when W == 0); next tile index published
+    __syncthreads();  // next tile index published
+    STAMP(0);
     const uint32_t next = a.dyn_tiles ? qs[1] : wg + G;
     // an empty filter (no chunks) has no batch to prefetch the next tile from
     if (W == 0 && next < total_tiles) fetch_rows(next, 0, pre_s, pre_e);
@@ -631,6 +651,7 @@ __global__ __launch_bounds__(kBlockB) void bloom_tile_kernel(BuildArgs a,
         if (i < nw) seg[i] = make_uint2(pos_base + (wb + i) * a.cap + rs[r], re[r] - rs[r]);
       }
       __syncthreads();  // segment list ready
+      STAMP(1);
       if (wb + kSegBatch >= W && next < total_tiles) fetch_rows(next, 0, pre_s, pre_e);
 
       const uint32_t Q = nw > (uint32_t)wave ? (nw - wave + NWAVES - 1) / NWAVES : 0;
@@ -696,6 +717,7 @@ __global__ __launch_bounds__(kBlockB) void bloom_tile_kernel(BuildArgs a,
         consume(B);
       }
       __syncthreads();  // segment list reused by the next batch; tile complete after the last
+      STAMP(2);
     }
 
     // Write the finished tile: bytes [lt << (TL-3), ...) of this filter, up to
@@ -705,14 +727,23 @@ __global__ __launch_bounds__(kBlockB) void bloom_tile_kernel(BuildArgs a,
     const uint64_t nbytes = min(tile_bytes, (uint64_t)d.alloc_bytes - b0);
     uint4 *out4 = reinterpret_cast<uint4 *>(bitmaps + d.bitmap_off + b0);
     const uint4 *t4 = reinterpret_cast<const uint4 *>(tile);
-    if (a.nt_bitmap) {
-      for (uint32_t i = tid; i < (uint32_t)(nbytes >> 4); i += kBlockB) store_nt(out4 + i, t4[i]);
-    } else {
-      for (uint32_t i = tid; i < (uint32_t)(nbytes >> 4); i += kBlockB) out4[i] = t4[i];
+    // Each 16-byte word is zeroed as it is read out (the whole tile, also past
+    // a short last tile), so the next tile needs no separate zeroing sweep.
+    uint4 *t4z = reinterpret_cast<uint4 *>(tile);
+    const uint32_t nvec = (uint32_t)(nbytes >> 4);
+    for (uint32_t i = tid; i < tile_words / 4; i += kBlockB) {
+      const uint4 v = t4[i];
+      t4z[i] = make_uint4(0, 0, 0, 0);
+      if (i < nvec) {
+        if (a.nt_bitmap) store_nt(out4 + i, v);
+        else out4[i] = v;
+      }
     }
-    __syncthreads();  // every lane has read the tile before the next one is zeroed
+    __syncthreads();  // the tile is read out and zero again
+    STAMP(3);
     wg = next;
   }
+  STAMP_FLUSH(1);
 }
 
 // ---------------------------------------------------------------- direct atomics
@@ -828,8 +859,8 @@ int make_plan(const uint64_t *counts, uint32_t nf, int32_t bpk, Plan &p) {
   p.a.nt_keys = env_flag("ADL_BLOOM_NT_KEYS", 1);
   p.a.nt_bitmap = env_flag("ADL_BLOOM_NT_BITMAP", 1);
   p.a.dyn_tiles = env_flag("ADL_BLOOM_DYN_TILES", 0);
-  p.a.inc_pos = env_flag("ADL_BLOOM_INC_POS", 0);
   p.a.stage_keys = env_flag("ADL_BLOOM_STAGE_KEYS", 1);
+  p.a.exp = env_u32("ADL_BLOOM_EXP", 0);
   p.a.k = k;
   p.a.C = C;
   p.a.TL = TL;
@@ -848,7 +879,6 @@ int make_plan(const uint64_t *counts, uint32_t nf, int32_t bpk, Plan &p) {
     d.tiles = (uint32_t)(((uint64_t)m + (1ull << TL) - 1) >> TL);
     if (d.tiles + 1 > kHistMax) return ADL_ERR_TOO_LARGE;
     d.mod = adl_host::make_fastmod(m);
-    d.wrap = (uint32_t)((1ull << 32) % m);
     d.chunk_base = chunk;
     d.tile_base = tile;
     d.pos_base = pos;
@@ -1034,6 +1064,16 @@ const char *adl_bloom_strerror(int status) {
 }
 
 int adl_bloom_abi_version(void) { return ADL_BLOOM_ABI_VERSION; }
+
+#ifdef ADL_BLOOM_STAMPS
+// Diagnostics build only: copies g_stamps ([pass][workgroup][phase] cycles).
+int adl_bloom_debug_stamps(uint64_t *out, uint64_t n) {
+  const uint64_t bytes = std::min<uint64_t>(n, 2 * 2048 * 8) * 8;
+  ADL_HIP_TRY(hipDeviceSynchronize());
+  ADL_HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), bytes, 0, hipMemcpyDeviceToHost));
+  return ADL_OK;
+}
+#endif
 
 int32_t adl_bloom_num_probes(int32_t bits_per_key) { return adl_host::num_probes(bits_per_key); }
 

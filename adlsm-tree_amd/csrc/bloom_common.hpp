@@ -126,15 +126,8 @@ namespace adl_host {
 inline adl_dev::FastMod make_fastmod(uint32_t m) {
   adl_dev::FastMod f{};
   f.m = m;
-  if ((m & (m - 1u)) == 0u) {
-    f.pow2 = 1;
-    f.magic = 0;
-    f.shift = 0;
-    return f;
-  }
   uint32_t l = 0;
-  while ((1ull << l) < m) ++l;  // ceil(log2 m)
-  f.pow2 = 0;
+  while ((1ull << l) < m) ++l;  // ceil(log2 m); m >= 2 (m = 8 * bitmap bytes >= 56)
   f.magic = (uint32_t)((((1ull << 32) * ((1ull << l) - m)) / m) + 1ull);
   f.shift = l - 1;
   return f;

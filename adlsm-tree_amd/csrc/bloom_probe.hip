@@ -75,7 +75,7 @@ __global__ __launch_bounds__(kBlockP) void bloom_probe_kernel(Keys keys, uint64_
 // constants of up to kLdsFilters filters are built once per workgroup into
 // LDS (dynamic, 8 B per filter), beyond that per query.
 struct ModLds {
-  uint32_t magic, shift_pow2;  // shift | pow2 << 8
+  uint32_t magic, shift;
 };
 
 template <class Keys>
@@ -88,7 +88,7 @@ __global__ __launch_bounds__(kBlockP) void bloom_probe_multi_kernel(
   if (lds_tab) {
     for (uint32_t f = threadIdx.x; f < nf; f += kBlockP) {
       const FastMod fm = fastmod_for((uint32_t)((boff[f + 1] - boff[f]) * 8));
-      lmod[f] = ModLds{fm.magic, fm.shift | (fm.pow2 << 8)};
+      lmod[f] = ModLds{fm.magic, fm.shift};
     }
     __syncthreads();
   }
@@ -103,7 +103,7 @@ __global__ __launch_bounds__(kBlockP) void bloom_probe_multi_kernel(
         FastMod mod;
         if (lds_tab) {
           const ModLds e = lmod[f];
-          mod = FastMod{m, e.magic, e.shift_pow2 & 0xffu, e.shift_pow2 >> 8};
+          mod = FastMod{m, e.magic, e.shift, 0u};
         } else {
           mod = fastmod_for(m);
         }

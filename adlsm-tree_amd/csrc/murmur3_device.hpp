@@ -153,11 +153,12 @@ __device__ __forceinline__ void hash_lds(const uint32_t *stage, uint32_t off, ui
   hb = fmix(b, len);
 }
 
-// h % m for a launch-constant divisor 1 <= m < 2^31 (Granlund-Montgomery
+// h % m for a launch-constant divisor 2 <= m < 2^31 (Granlund-Montgomery
 // round-up method, exact for every 32-bit numerator): q = (t + ((h-t)>>1)) >> (l-1),
-// t = mulhi(h, magic).  For m a power of two (l == 0 path) magic = 0, shift = log2 m.
+// t = mulhi(h, magic), l = ceil(log2 m).  A power of two m = 2^l gets magic = 1
+// (t = 0, q = h >> l), so one branch-free sequence covers every divisor.
 struct FastMod {
-  uint32_t m, magic, shift, pow2;
+  uint32_t m, magic, shift, pad_;
 };
 
 // Device-side construction (same values as adl_host::make_fastmod); for
@@ -165,19 +166,14 @@ struct FastMod {
 __device__ __forceinline__ FastMod fastmod_for(uint32_t m) {
   FastMod f;
   f.m = m;
-  if ((m & (m - 1u)) == 0u) {
-    f.pow2 = 1; f.magic = 0; f.shift = 0;
-    return f;
-  }
-  const uint32_t l = 32u - __clz(m - 1u);  // ceil(log2 m), m >= 3
-  f.pow2 = 0;
+  f.pad_ = 0;
+  const uint32_t l = 32u - __clz(m - 1u);  // ceil(log2 m), m >= 2
   f.magic = (uint32_t)((((1ull << 32) * ((1ull << l) - m)) / m) + 1ull);
   f.shift = l - 1u;
   return f;
 }
 
 __device__ __forceinline__ uint32_t fastmod(uint32_t h, const FastMod &d) {
-  if (d.pow2) return h & (d.m - 1u);
   const uint32_t t = __umulhi(h, d.magic);
   const uint32_t q = (t + ((h - t) >> 1)) >> d.shift;
   return h - q * d.m;

@@ -1,0 +1,52 @@
+"""tools/stamps.py -- per-phase cycle breakdown of the two build kernels.
+
+Loads the s_memtime-instrumented library (make -C adlsm-tree_amd stamps),
+runs the 10M x 16B headline build a few times and prints, per pass, the mean
+over workgroups of the cycles wave 0 spent in each phase (phase = the span
+between two of the kernel's barriers; see STAMP() in csrc/bloom_build.hip).
+Diagnostics only; never part of the product path.
+"""
+import ctypes
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+os.environ["ADL_BLOOM_LIB"] = os.path.join(ROOT, "adlsm-tree_amd", "lib_stamps", "libadlbloom.so")
+sys.path.insert(0, os.path.join(ROOT, "adlsm-tree_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import adlbloom  # noqa: E402
+
+NAMES = {
+    0: ["loop-top (clear, hash)", "count+store(prev)", "scan", "table", "scatter", "epilogue", "-", "-"],
+    1: ["tile start", "stage segs", "gather+or", "write+zero tile", "-", "-", "-", "-"],
+}
+
+
+def main():
+    n = int(os.environ.get("N", 10_000_000))
+    keys = adlbloom.synth_keys16(n, seed=0x5EED, device="cuda:0")
+    for _ in range(3):
+        bm = adlbloom.build(keys, bits_per_key=10)
+    torch.cuda.synchronize()
+    L = adlbloom.lib()
+    L.adl_bloom_debug_stamps.restype = ctypes.c_int
+    L.adl_bloom_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
+    buf = np.zeros((2, 2048, 8), dtype=np.uint64)
+    assert L.adl_bloom_debug_stamps(buf.ctypes.data, buf.size) == 0
+    for p in (0, 1):
+        rows = buf[p][buf[p].sum(axis=1) > 0]
+        tot = rows.sum(axis=1).mean()
+        print(f"pass {'AB'[p]}: {len(rows)} workgroups, mean total {tot:.0f} cycles")
+        for i in range(8):
+            if NAMES[p][i] == "-":
+                continue
+            col = rows[:, i].astype(np.float64)
+            print(f"  {NAMES[p][i]:22s} mean {col.mean():9.0f}  max {col.max():9.0f}  ({100 * col.mean() / tot:5.1f} %)")
+    del bm
+
+
+if __name__ == "__main__":
+    main()
