@@ -33,6 +33,7 @@ EXPORTS = (
     "adl_bloom_strerror", "adl_bloom_abi_version", "adl_bloom_num_probes",
     "adl_bloom_bitmap_bytes", "adl_bloom_bitmap_alloc_bytes", "adl_bloom_build_workspace_bytes",
     "adl_bloom_build_device", "adl_bloom_build_segmented_device", "adl_bloom_build",
+    "adl_bloom_build_segmented",
     "adl_bloom_probe_device", "adl_bloom_probe_multi_device", "adl_bloom_probe",
     "adl_bloom_filter_set_create", "adl_bloom_filter_set_probe",
     "adl_bloom_filter_set_device_view", "adl_bloom_filter_set_destroy",
@@ -70,6 +71,7 @@ def lib() -> ctypes.CDLL:
         "adl_bloom_build_device": (ctypes.c_int, [vp, vp, u64, u32, i32, vp, vp, u64, vp]),
         "adl_bloom_build_segmented_device": (ctypes.c_int, [vp, vp, u32, vp, u32, i32, vp, vp, vp, u64, vp]),
         "adl_bloom_build": (ctypes.c_int, [vp, vp, u64, u32, i32, vp, vp]),
+        "adl_bloom_build_segmented": (ctypes.c_int, [vp, vp, u32, vp, u32, i32, vp, vp, vp]),
         "adl_bloom_probe_device": (ctypes.c_int, [vp, vp, u64, u32, i32, vp, u64, vp, vp]),
         "adl_bloom_probe_multi_device": (ctypes.c_int, [vp, vp, u64, u32, vp, u32, vp, vp, i32, vp, vp]),
         "adl_bloom_probe": (ctypes.c_int, [vp, vp, u64, u32, i32, vp, u64, vp, vp]),
@@ -231,6 +233,28 @@ def build_segmented(keys, key_begin, offsets=None, bits_per_key: int = 10, strea
                                                   _stream(stream)), "adl_bloom_build_segmented_device")
     torch.cuda.current_stream().synchronize()  # ws/out lifetimes end with this call's tensors
     return out, boff, sizes
+
+
+def _host_ptr(a):
+    """Host address of a numpy array or a CPU (possibly pinned) torch tensor."""
+    if isinstance(a, np.ndarray):
+        return a.ctypes.data
+    assert not a.is_cuda, "host buffer expected"
+    return a.data_ptr()
+
+
+def build_segmented_host(keys, key_begin, out, bitmap_off, offsets=None, bits_per_key: int = 10, stream=None):
+    """Host-pointer pipelined segmented build (adl_bloom_build_segmented):
+    keys (n, stride) uint8 or packed bytes + offsets (n+1) in host memory
+    (numpy, or CPU torch tensors -- pinned ones are DMAed directly); filter f's
+    exact-length bitmap lands at out[bitmap_off[f]:] (out: host uint8 buffer)."""
+    kb = np.ascontiguousarray(key_begin, dtype=np.uint64)
+    bo = np.ascontiguousarray(bitmap_off, dtype=np.uint64)
+    stride = 0 if offsets is not None else int(keys.shape[1])
+    _check(lib().adl_bloom_build_segmented(_host_ptr(keys), None if offsets is None else _host_ptr(offsets),
+                                           stride, kb.ctypes.data, len(kb) - 1, bits_per_key, _host_ptr(out),
+                                           bo.ctypes.data, _stream(stream)), "adl_bloom_build_segmented")
+    return out
 
 
 def probe(keys, bitmap, nbytes: int | None = None, offsets=None, bits_per_key: int = 10, stream=None):

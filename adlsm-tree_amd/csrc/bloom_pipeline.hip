@@ -1,0 +1,258 @@
+// adlsm-tree_amd/csrc/bloom_pipeline.hip -- host-pointer segmented build,
+// pipelined over three HIP streams (adl_bloom_build_segmented).
+//
+// The compaction-shaped producer of the reference (MergeRuns emitting many
+// SSTables, src/db.cpp:428-509, each finalised by SSTableWriter::Final ->
+// FilterBlockWriter::Final, src/sstable.cpp:58) hands over keys in host
+// memory and wants the bitmaps back in host memory.  The filters are taken in
+// groups (<= kGroupFilters filters, <= kGroupKeyBytes of keys); group g's keys
+// upload on one stream while group g-1 builds on the caller's stream and group
+// g-2's bitmaps download on a third, so the end-to-end rate approaches the
+// slower PCIe direction instead of the sum of both plus the kernels.
+// Pageable caller memory is staged through per-thread pinned double buffers
+// (the CPU copy of group g+1 overlaps the DMAs of group g); pinned caller
+// memory is DMAed directly.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "bloom_common.hpp"
+
+namespace {
+
+constexpr uint32_t kGroupFilters = 8;               // filters per launch pair (bloom_build.hip kMaxFilters)
+constexpr uint64_t kGroupKeyBytes = 32ull << 20;    // keys per group, soft cap (at least one filter)
+
+bool is_pinned(const void *p) {
+  if (!p) return false;
+  hipPointerAttribute_t attr;
+  if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
+    (void)hipGetLastError();  // pageable memory: clear the sticky error
+    return false;
+  }
+  return attr.type == hipMemoryTypeHost;
+}
+
+// Per-thread buffers, grown on demand and reused (the C-ABI stays re-entrant).
+struct Pipe {
+  hipStream_t up = nullptr, down = nullptr;
+  hipEvent_t ev_up[2] = {}, ev_built[2] = {}, ev_down[2] = {};
+  bool used_up[2] = {}, used_down[2] = {};
+  uint8_t *h_in[2] = {}, *h_out[2] = {}, *d_in[2] = {}, *d_out[2] = {}, *d_ws = nullptr;
+  uint64_t h_in_cap = 0, h_out_cap = 0, d_in_cap = 0, d_out_cap = 0, ws_cap = 0;
+
+  ~Pipe() {
+    for (int b = 0; b < 2; ++b) {
+      if (h_in[b]) (void)hipHostFree(h_in[b]);
+      if (h_out[b]) (void)hipHostFree(h_out[b]);
+      if (d_in[b]) (void)hipFree(d_in[b]);
+      if (d_out[b]) (void)hipFree(d_out[b]);
+      if (ev_up[b]) (void)hipEventDestroy(ev_up[b]);
+      if (ev_built[b]) (void)hipEventDestroy(ev_built[b]);
+      if (ev_down[b]) (void)hipEventDestroy(ev_down[b]);
+    }
+    if (d_ws) (void)hipFree(d_ws);
+    if (up) (void)hipStreamDestroy(up);
+    if (down) (void)hipStreamDestroy(down);
+  }
+
+  int init() {
+    if (up) return ADL_OK;
+    ADL_HIP_TRY(hipStreamCreateWithFlags(&up, hipStreamNonBlocking));
+    ADL_HIP_TRY(hipStreamCreateWithFlags(&down, hipStreamNonBlocking));
+    for (int b = 0; b < 2; ++b) {
+      ADL_HIP_TRY(hipEventCreateWithFlags(&ev_up[b], hipEventDisableTiming));
+      ADL_HIP_TRY(hipEventCreateWithFlags(&ev_built[b], hipEventDisableTiming));
+      ADL_HIP_TRY(hipEventCreateWithFlags(&ev_down[b], hipEventDisableTiming));
+    }
+    return ADL_OK;
+  }
+
+  // Grow a pair of buffers; callers have drained every use of them first.
+  static int grow(uint8_t *(&buf)[2], uint64_t &cap, uint64_t want, bool pinned) {
+    if (want <= cap) return ADL_OK;
+    for (int b = 0; b < 2; ++b) {
+      if (buf[b]) (void)(pinned ? hipHostFree(buf[b]) : hipFree(buf[b]));
+      buf[b] = nullptr;
+    }
+    cap = 0;
+    const uint64_t sz = adl_host::round_up(want + (want >> 3), 1 << 16);
+    for (int b = 0; b < 2; ++b) {
+      const hipError_t e = pinned ? hipHostMalloc((void **)&buf[b], sz, hipHostMallocDefault)
+                                  : hipMalloc((void **)&buf[b], sz);
+      if (e != hipSuccess) return ADL_ERR_OUT_OF_MEMORY;
+    }
+    cap = sz;
+    return ADL_OK;
+  }
+};
+
+thread_local Pipe t_pipe;
+
+struct Group {
+  uint32_t f0, f1;       // filters [f0, f1)
+  uint64_t b0, b1;       // key bytes [b0, b1) uploaded (b0 16-byte aligned down)
+  uint64_t k0, k1;       // keys [k0, k1)
+  uint64_t off_bytes;    // offsets uploaded ((k1-k0+1)*8, var-len only)
+  uint64_t out_bytes;    // device bitmap bytes (16-byte aligned per filter)
+  uint64_t ws;           // workspace
+};
+
+}  // namespace
+
+extern "C" int adl_bloom_build_segmented(const uint8_t *h_keys, const uint64_t *h_offsets, uint32_t key_stride,
+                                         const uint64_t *key_begin, uint32_t num_filters, int32_t bits_per_key,
+                                         uint8_t *h_bitmaps, const uint64_t *h_bitmap_off, void *stream) {
+  try {
+    if (!key_begin || !h_bitmap_off || !h_bitmaps || num_filters == 0) return ADL_ERR_INVALID_ARG;
+    if (bits_per_key < 0) return ADL_ERR_INVALID_ARG;
+    if (!h_offsets && key_stride == 0 && key_begin[num_filters] > key_begin[0]) return ADL_ERR_INVALID_ARG;
+    if (!h_keys && key_begin[num_filters] > key_begin[0]) return ADL_ERR_INVALID_ARG;
+    for (uint32_t f = 0; f < num_filters; ++f) {
+      if (key_begin[f + 1] < key_begin[f]) return ADL_ERR_INVALID_ARG;
+      if (adl_host::bitmap_bytes(key_begin[f + 1] - key_begin[f], bits_per_key) == 0) return ADL_ERR_TOO_LARGE;
+    }
+    auto key_byte = [&](uint64_t k) -> uint64_t { return h_offsets ? h_offsets[k] : k * (uint64_t)key_stride; };
+
+    // groups of consecutive filters
+    std::vector<Group> groups;
+    uint64_t max_in = 0, max_out = 0, max_ws = 0;
+    for (uint32_t f0 = 0; f0 < num_filters;) {
+      Group g{};
+      g.f0 = f0;
+      uint32_t f1 = f0 + 1;
+      while (f1 < num_filters && f1 - f0 < kGroupFilters &&
+             key_byte(key_begin[f1 + 1]) - key_byte(key_begin[f0]) <= kGroupKeyBytes)
+        ++f1;
+      g.f1 = f1;
+      g.k0 = key_begin[f0];
+      g.k1 = key_begin[f1];
+      g.b0 = key_byte(g.k0) & ~15ull;
+      g.b1 = key_byte(g.k1);
+      g.off_bytes = h_offsets ? (g.k1 - g.k0 + 1) * 8 : 0;
+      std::vector<uint64_t> counts;
+      for (uint32_t f = f0; f < f1; ++f) {
+        const uint64_t n = key_begin[f + 1] - key_begin[f];
+        counts.push_back(n);
+        g.out_bytes += adl_host::round_up(adl_host::bitmap_bytes(n, bits_per_key), 16);
+      }
+      g.ws = adl_bloom_build_workspace_bytes(counts.data(), (uint32_t)counts.size(), bits_per_key);
+      if (!g.ws) return ADL_ERR_TOO_LARGE;
+      max_in = std::max(max_in, adl_host::round_up(g.b1 - g.b0, 256) + g.off_bytes);
+      max_out = std::max(max_out, g.out_bytes);
+      max_ws = std::max(max_ws, g.ws);
+      groups.push_back(g);
+      f0 = f1;
+    }
+
+    Pipe &P = t_pipe;
+    if (int rc = P.init()) return rc;
+    hipStream_t comp = (hipStream_t)stream;
+    // earlier calls on this thread left nothing in flight (each call drains)
+    const bool pin_in = is_pinned(h_keys) && (!h_offsets || is_pinned(h_offsets));
+    const bool pin_out = is_pinned(h_bitmaps);
+    if (int rc = Pipe::grow(P.d_in, P.d_in_cap, max_in, false)) return rc;
+    if (int rc = Pipe::grow(P.d_out, P.d_out_cap, max_out, false)) return rc;
+    if (!pin_in)
+      if (int rc = Pipe::grow(P.h_in, P.h_in_cap, max_in, true)) return rc;
+    if (!pin_out)
+      if (int rc = Pipe::grow(P.h_out, P.h_out_cap, max_out, true)) return rc;
+    if (max_ws > P.ws_cap) {
+      if (P.d_ws) (void)hipFree(P.d_ws);
+      P.d_ws = nullptr;
+      P.ws_cap = 0;
+      ADL_HIP_TRY(hipMalloc((void **)&P.d_ws, max_ws));
+      P.ws_cap = max_ws;
+    }
+    P.used_up[0] = P.used_up[1] = P.used_down[0] = P.used_down[1] = false;
+
+    std::vector<uint64_t> local_kb, dev_off;
+    // host side of a finished group: copy its bitmaps out of the pinned staging
+    auto finish = [&](const Group &g) -> int {
+      if (pin_out) return ADL_OK;
+      const int b = (int)(&g - groups.data()) & 1;
+      ADL_HIP_TRY(hipEventSynchronize(P.ev_down[b]));
+      uint64_t o = 0;
+      for (uint32_t f = g.f0; f < g.f1; ++f) {
+        const uint64_t bytes = adl_host::bitmap_bytes(key_begin[f + 1] - key_begin[f], bits_per_key);
+        memcpy(h_bitmaps + h_bitmap_off[f], P.h_out[b] + o, bytes);
+        o += adl_host::round_up(bytes, 16);
+      }
+      return ADL_OK;
+    };
+
+    for (size_t gi = 0; gi < groups.size(); ++gi) {
+      const Group &g = groups[gi];
+      const int b = (int)(gi & 1);
+      const uint64_t kb = g.b1 - g.b0, kb_al = adl_host::round_up(kb, 256);
+      // 1. upload (buffers of group gi-2 are free once its build has run)
+      const uint8_t *src_keys = h_keys + g.b0;
+      const uint8_t *src_offs = reinterpret_cast<const uint8_t *>(h_offsets ? h_offsets + g.k0 : nullptr);
+      if (!pin_in) {
+        if (P.used_up[b]) ADL_HIP_TRY(hipEventSynchronize(P.ev_up[b]));
+        if (kb) memcpy(P.h_in[b], src_keys, kb);
+        if (g.off_bytes) memcpy(P.h_in[b] + kb_al, src_offs, g.off_bytes);
+        src_keys = P.h_in[b];
+        src_offs = P.h_in[b] + kb_al;
+      }
+      if (P.used_up[b]) ADL_HIP_TRY(hipStreamWaitEvent(P.up, P.ev_built[b], 0));
+      if (kb) ADL_HIP_TRY(hipMemcpyAsync(P.d_in[b], src_keys, kb, hipMemcpyHostToDevice, P.up));
+      if (g.off_bytes)
+        ADL_HIP_TRY(hipMemcpyAsync(P.d_in[b] + kb_al, src_offs, g.off_bytes, hipMemcpyHostToDevice, P.up));
+      ADL_HIP_TRY(hipEventRecord(P.ev_up[b], P.up));
+      P.used_up[b] = true;
+
+      // 2. build on the caller's stream once the keys are in and the output
+      //    buffer's previous bitmaps have downloaded.  Var-len offsets stay
+      //    absolute: the key pointer is shifted back by the group's first byte.
+      ADL_HIP_TRY(hipStreamWaitEvent(comp, P.ev_up[b], 0));
+      if (P.used_down[b]) ADL_HIP_TRY(hipStreamWaitEvent(comp, P.ev_down[b], 0));
+      local_kb.assign(g.f1 - g.f0 + 1, 0);
+      dev_off.assign(g.f1 - g.f0, 0);
+      uint64_t o = 0;
+      for (uint32_t f = g.f0; f <= g.f1; ++f) local_kb[f - g.f0] = key_begin[f] - g.k0;
+      for (uint32_t f = g.f0; f < g.f1; ++f) {
+        dev_off[f - g.f0] = o;
+        o += adl_host::round_up(adl_host::bitmap_bytes(key_begin[f + 1] - key_begin[f], bits_per_key), 16);
+      }
+      const uint8_t *d_keys = h_offsets ? P.d_in[b] - g.b0 : P.d_in[b];
+      const uint64_t *d_offs = h_offsets ? reinterpret_cast<const uint64_t *>(P.d_in[b] + kb_al) : nullptr;
+      if (int rc = adl_bloom_build_segmented_device(d_keys, d_offs, key_stride, local_kb.data(), g.f1 - g.f0,
+                                                    bits_per_key, P.d_out[b], dev_off.data(), P.d_ws, P.ws_cap,
+                                                    comp)) {
+        (void)hipDeviceSynchronize();
+        return rc;
+      }
+      ADL_HIP_TRY(hipEventRecord(P.ev_built[b], comp));
+
+      // 3. download after the build
+      ADL_HIP_TRY(hipStreamWaitEvent(P.down, P.ev_built[b], 0));
+      if (pin_out) {
+        for (uint32_t f = g.f0; f < g.f1; ++f) {
+          const uint64_t bytes = adl_host::bitmap_bytes(key_begin[f + 1] - key_begin[f], bits_per_key);
+          ADL_HIP_TRY(hipMemcpyAsync(h_bitmaps + h_bitmap_off[f], P.d_out[b] + dev_off[f - g.f0], bytes,
+                                     hipMemcpyDeviceToHost, P.down));
+        }
+      } else {
+        if (P.used_down[b] && gi >= 2) ADL_HIP_TRY(hipEventSynchronize(P.ev_down[b]));  // h_out[b] copied out
+        ADL_HIP_TRY(hipMemcpyAsync(P.h_out[b], P.d_out[b], g.out_bytes, hipMemcpyDeviceToHost, P.down));
+      }
+      ADL_HIP_TRY(hipEventRecord(P.ev_down[b], P.down));
+      P.used_down[b] = true;
+
+      // 4. meanwhile the host copies out the previous group's bitmaps
+      if (gi >= 1)
+        if (int rc = finish(groups[gi - 1])) return rc;
+    }
+    if (int rc = finish(groups.back())) return rc;
+    ADL_HIP_TRY(hipStreamSynchronize(P.down));
+    ADL_HIP_TRY(hipStreamSynchronize(P.up));
+    ADL_HIP_TRY(hipStreamSynchronize(comp));
+    return ADL_OK;
+  } catch (...) {
+    return ADL_ERR_DEVICE;
+  }
+}

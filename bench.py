@@ -327,6 +327,51 @@ def e2e(n, iters=5):
             "h2d_bytes": n * 16, "d2h_bytes": b.nbytes, "host_memory": "pinned"}
 
 
+def e2e_compaction(w, iters=3):
+    """Compaction shape end to end: 32 tables' keys in pinned host memory ->
+    adl_bloom_build_segmented (groups of filters: key upload, build and bitmap
+    download overlapped on three streams) -> exact-length bitmaps packed back
+    to back in pinned host memory (the filter-block layout).  Also times the
+    unpipelined sequence (all keys up, one segmented build, all bitmaps down)."""
+    import numpy as np
+    import torch
+
+    import adlbloom as ab
+
+    kb = w.builder.kb
+    n = int(kb[-1])
+    keys_h = torch.empty((n, 16), dtype=torch.uint8, pin_memory=True)
+    keys_h.copy_(w.keys)
+    sizes = [ab.bitmap_bytes(int(kb[f + 1] - kb[f]), BPK) for f in range(len(kb) - 1)]
+    boff = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.uint64)
+    out_h = torch.zeros(int(sum(sizes)), dtype=torch.uint8, pin_memory=True)
+    ab.build_segmented_host(keys_h, kb, out_h, boff)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        ab.build_segmented_host(keys_h, kb, out_h, boff)
+    dt = (time.perf_counter() - t0) / iters
+    # unpipelined: H2D all keys, one segmented build, D2H the device bitmaps
+    dst = torch.empty_like(w.keys)
+    seq_h = torch.empty(w.builder.out.numel(), dtype=torch.uint8, pin_memory=True)
+
+    def seq():
+        dst.copy_(keys_h, non_blocking=True)
+        out = w.builder.build(dst)
+        seq_h.copy_(out, non_blocking=True)
+        torch.cuda.current_stream().synchronize()
+
+    seq()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        seq()
+    ds = (time.perf_counter() - t0) / iters
+    return {"value": round(n / dt / 1e6, 1), "unit": "Mkeys/s", "ms_per_build": round(dt * 1e3, 3),
+            "h2d_bytes": n * 16, "d2h_bytes": int(sum(sizes)), "host_memory": "pinned",
+            "api": "adl_bloom_build_segmented (pipelined groups)",
+            "unpipelined": {"value": round(n / ds / 1e6, 1), "ms_per_build": round(ds * 1e3, 3)}}
+
+
 def parity_check(bm_dev, n):
     """Rank-0 bitmap vs the reference's SHA-256 for the seed-0x5EED key set."""
     path = os.path.join(ROOT, "tests", "golden", "appendix_b.json")
@@ -463,6 +508,8 @@ def main():
         }
         if world == 1 and args.workload == "single" and not args.no_e2e:
             out_json["e2e"] = e2e(w.n)
+        if world == 1 and args.workload == "compaction" and not args.no_e2e:
+            out_json["e2e"] = e2e_compaction(w)
         if world == 1 and not args.no_cpu_baseline:
             out_json["cpu_baseline"] = cpu_baseline(args.cpu_seconds, args.workload, w)
         else:

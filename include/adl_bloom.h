@@ -103,6 +103,21 @@ int adl_bloom_build(const uint8_t *h_keys, const uint64_t *h_offsets, uint64_t n
                     uint32_t key_stride, int32_t bits_per_key, uint8_t *h_bitmap,
                     void *stream);
 
+/* Host-pointer segmented build for many filters (the compaction shape: one
+ * filter per SSTable, keys and bitmaps in host memory), pipelined: filters go
+ * in groups (<= 8 filters, ~32 MB of keys) whose key upload, build (on
+ * `stream`) and bitmap download overlap on three streams.  Filter f's bitmap,
+ * exactly adl_bloom_bitmap_bytes(n_f, bpk) bytes, is written at
+ * h_bitmaps + h_bitmap_off[f] (any alignment, e.g. packed back to back as in
+ * a filter block).  Pinned (hipHostMalloc'd / registered) buffers are DMAed
+ * directly; pageable ones are staged through per-thread pinned buffers.
+ * key_begin (num_filters+1) and h_bitmap_off (num_filters) are HOST arrays.
+ * Synchronous.  Replaces num_filters calls of BloomFilter::Keys2Block
+ * (src/filter_block.cpp:9-33) from SSTableWriter::Final (src/sstable.cpp:58). */
+int adl_bloom_build_segmented(const uint8_t *h_keys, const uint64_t *h_offsets, uint32_t key_stride,
+                              const uint64_t *key_begin, uint32_t num_filters, int32_t bits_per_key,
+                              uint8_t *h_bitmaps, const uint64_t *h_bitmap_off, void *stream);
+
 /* ---------------------------------------------------------------- probe */
 
 /* Probe n keys against one device bitmap of bitmap_bytes bytes (the exact

@@ -245,6 +245,44 @@ def test_build_compaction_shape_32_tables(dev, ab, oracle):
         assert np.array_equal(got, oracle.keys2block(oracle.splitmix_keys16(0x5EED + t, n))), t
 
 
+@pytest.mark.parametrize("pinned", [False, True])
+def test_build_segmented_host_pipelined(dev, ab, oracle, pinned):
+    # adl_bloom_build_segmented: host keys -> pipelined groups -> host bitmaps packed
+    # back to back at unaligned offsets (the filter-block layout).  Sizes span
+    # several groups (<= 8 filters / ~32 MB of keys each, a 2.5M-key filter alone
+    # past the cap), empty filters and 1-key filters.
+    sizes = [0, 1, 1000, 50_000, 7, 2_500_000, 6144, 6145, 3, 200_000, 10, 99_999, 2, 0, 300_000, 17]
+    kb = np.concatenate([[0], np.cumsum(sizes)]).astype(np.uint64)
+    hk = oracle.splitmix_keys16(77, int(kb[-1]))
+    nbytes = [ab.bitmap_bytes(n, 10) for n in sizes]
+    boff = np.concatenate([[0], np.cumsum(nbytes)[:-1]]).astype(np.uint64)
+    total = int(sum(nbytes))
+    if pinned:
+        keys = dev.from_numpy(hk).pin_memory()
+        out = dev.zeros(total, dtype=dev.uint8).pin_memory()
+    else:
+        keys, out = hk, np.zeros(total, dtype=np.uint8)
+    ab.build_segmented_host(keys, kb, out, boff)
+    out = out.numpy() if pinned else out
+    for f, n in enumerate(sizes):
+        want = oracle.keys2block(hk[kb[f]:kb[f + 1]])
+        assert np.array_equal(out[int(boff[f]):int(boff[f]) + nbytes[f]], want), f
+
+
+def test_build_segmented_host_varlen(dev, ab, oracle):
+    rng = random.Random(9)
+    keys = rand_keys(rng, 30000, 0, 80)
+    data, offs = oracle.pack(keys)
+    kb = np.array([0, 1, 7000, 7000, 18000, 30000], dtype=np.uint64)
+    nbytes = [ab.bitmap_bytes(int(kb[f + 1] - kb[f]), 10) for f in range(5)]
+    boff = np.concatenate([[0], np.cumsum(nbytes)[:-1]]).astype(np.uint64)
+    out = np.zeros(int(sum(nbytes)), dtype=np.uint8)
+    ab.build_segmented_host(np.concatenate([data, np.zeros(16, np.uint8)]), kb, out, boff, offsets=offs)
+    for f in range(5):
+        want = oracle.keys2block(keys[int(kb[f]):int(kb[f + 1])])
+        assert np.array_equal(out[int(boff[f]):int(boff[f]) + nbytes[f]], want), f
+
+
 # ----------------------------------------------------------------- probe
 def test_probe_matches_appendix_b(dev, ab, golden, oracle):
     for g in golden["appendix_b"]["probes"]:
