@@ -23,6 +23,7 @@
 //
 // A direct device-scope atomicOr kernel (bloom_atomic_kernel) is kept as the
 // alternative for small filters and as an independent cross-check.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -860,7 +861,11 @@ int make_plan(const uint64_t *counts, uint32_t nf, int32_t bpk, Plan &p) {
   p.a.nt_bitmap = env_flag("ADL_BLOOM_NT_BITMAP", 1);
   p.a.dyn_tiles = env_flag("ADL_BLOOM_DYN_TILES", 0);
   p.a.stage_keys = env_flag("ADL_BLOOM_STAGE_KEYS", 1);
-  p.a.exp = env_u32("ADL_BLOOM_EXP", 0);
+#ifdef ADL_BLOOM_STAMPS
+  p.a.exp = env_u32("ADL_BLOOM_EXP", 0);  // diagnostics build only
+#else
+  p.a.exp = 0;
+#endif
   p.a.k = k;
   p.a.C = C;
   p.a.TL = TL;
@@ -917,11 +922,13 @@ bool use_atomic_path() {
 }
 
 // ---------------------------------------------------------------- instrumentation
-// Thread-local event triples (before pass A, between A and B, after B).
+// Thread-local event quadruples: start/stop of pass A and of pass B, taken
+// from the kernels' own dispatch packets (hipExtLaunchKernel), so profiling
+// adds no marker packets -- and no gaps -- between the launches.
 struct Profile {
   bool on = false;
   uint32_t used = 0;
-  std::vector<hipEvent_t> ev;  // 3 per build
+  std::vector<hipEvent_t> ev;  // 4 per build
   ~Profile() {
     for (hipEvent_t e : ev) (void)hipEventDestroy(e);
   }
@@ -929,8 +936,8 @@ struct Profile {
 thread_local Profile t_prof;
 
 inline hipEvent_t *prof_slot() {
-  if (!t_prof.on || 3 * (t_prof.used + 1) > t_prof.ev.size()) return nullptr;
-  return &t_prof.ev[3 * t_prof.used++];
+  if (!t_prof.on || 4 * (t_prof.used + 1) > t_prof.ev.size()) return nullptr;
+  return &t_prof.ev[4 * t_prof.used++];
 }
 
 template <class Keys>
@@ -939,13 +946,16 @@ int launch_binned(const Plan &p, Keys keys, uint8_t *d_bitmaps, void *ws, hipStr
   uint32_t *tab_ws = pos_ws + p.pos_words;
   uint32_t *queue = tab_ws + p.table_words;  // pass B tile queue, then pass A's scratch lines
   hipEvent_t *ev = prof_slot();
-  if (ev) ADL_HIP_TRY(hipEventRecord(ev[0], st));
+  if (ev && !p.total_chunks) {  // no pass A: an empty interval
+    ADL_HIP_TRY(hipEventRecord(ev[0], st));
+    ADL_HIP_TRY(hipEventRecord(ev[1], st));
+  }
   if (p.total_chunks) {
     auto go = [&](auto kern) -> int {
       ADL_HIP_TRY(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                                       (int)p.lds_a));
-      hipLaunchKernelGGL(kern, dim3(p.grid_a), dim3(p.block_a), p.lds_a, st, p.a, keys, pos_ws, tab_ws,
-                         p.total_chunks, queue);
+      hipExtLaunchKernelGGL(kern, dim3(p.grid_a), dim3(p.block_a), p.lds_a, st, ev ? ev[0] : nullptr,
+                            ev ? ev[1] : nullptr, 0, p.a, keys, pos_ws, tab_ws, p.total_chunks, queue);
       ADL_HIP_TRY(hipGetLastError());
       return ADL_OK;
     };
@@ -961,13 +971,13 @@ int launch_binned(const Plan &p, Keys keys, uint8_t *d_bitmaps, void *ws, hipStr
                                      : by_block(std::integral_constant<int, 512>{}, 0);
     if (rc) return rc;
   }
-  if (ev) ADL_HIP_TRY(hipEventRecord(ev[1], st));
   auto go_b = [&](auto kern) -> int {
     ADL_HIP_TRY(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)p.lds_b));
     BuildArgs ab = p.a;
     if (!p.total_chunks) ab.dyn_tiles = 0;  // no pass A ran to reset the queue
-    hipLaunchKernelGGL(kern, dim3(p.grid_b), dim3(kBlockB), p.lds_b, st, ab, (const uint32_t *)pos_ws,
-                       (const uint32_t *)tab_ws, d_bitmaps, p.total_tiles, queue);
+    hipExtLaunchKernelGGL(kern, dim3(p.grid_b), dim3(kBlockB), p.lds_b, st, ev ? ev[2] : nullptr,
+                          ev ? ev[3] : nullptr, 0, ab, (const uint32_t *)pos_ws, (const uint32_t *)tab_ws,
+                          d_bitmaps, p.total_tiles, queue);
     ADL_HIP_TRY(hipGetLastError());
     return ADL_OK;
   };
@@ -976,9 +986,7 @@ int launch_binned(const Plan &p, Keys keys, uint8_t *d_bitmaps, void *ws, hipStr
   else if (p.depth <= 6) rcb = go_b(bloom_tile_kernel<6>);
   else if (p.depth <= 8) rcb = go_b(bloom_tile_kernel<8>);
   else rcb = go_b(bloom_tile_kernel<12>);
-  if (rcb) return rcb;
-  if (ev) ADL_HIP_TRY(hipEventRecord(ev[2], st));
-  return ADL_OK;
+  return rcb;
 }
 
 template <class Keys>
@@ -1170,7 +1178,7 @@ int adl_bloom_build(const uint8_t *h_keys, const uint64_t *h_offsets, uint64_t n
 
 int adl_bloom_profile_enable(uint32_t capacity) {
   try {
-    while (t_prof.ev.size() < 3ull * capacity) {
+    while (t_prof.ev.size() < 4ull * capacity) {
       hipEvent_t e;
       ADL_HIP_TRY(hipEventCreate(&e));
       t_prof.ev.push_back(e);
@@ -1187,11 +1195,11 @@ int adl_bloom_profile_collect(double *ms, uint32_t *builds) {
   if (!ms || !builds) return ADL_ERR_INVALID_ARG;
   ms[0] = ms[1] = 0.0;
   for (uint32_t i = 0; i < t_prof.used; ++i) {
-    hipEvent_t *e = &t_prof.ev[3 * i];
+    hipEvent_t *e = &t_prof.ev[4 * i];
     float a = 0.f, b = 0.f;
-    ADL_HIP_TRY(hipEventSynchronize(e[2]));
+    ADL_HIP_TRY(hipEventSynchronize(e[3]));
     ADL_HIP_TRY(hipEventElapsedTime(&a, e[0], e[1]));
-    ADL_HIP_TRY(hipEventElapsedTime(&b, e[1], e[2]));
+    ADL_HIP_TRY(hipEventElapsedTime(&b, e[2], e[3]));
     ms[0] += a;
     ms[1] += b;
   }
