@@ -33,7 +33,8 @@ EXPORTS = (
     "adl_bloom_strerror", "adl_bloom_abi_version", "adl_bloom_num_probes",
     "adl_bloom_bitmap_bytes", "adl_bloom_bitmap_alloc_bytes", "adl_bloom_build_workspace_bytes",
     "adl_bloom_build_device", "adl_bloom_build_segmented_device", "adl_bloom_build",
-    "adl_bloom_build_segmented",
+    "adl_bloom_build_segmented", "adl_bloom_filter_block_bytes", "adl_bloom_filter_block_workspace_bytes",
+    "adl_bloom_filter_block_build_device",
     "adl_bloom_probe_device", "adl_bloom_probe_multi_device", "adl_bloom_probe",
     "adl_bloom_filter_set_create", "adl_bloom_filter_set_probe",
     "adl_bloom_filter_set_device_view", "adl_bloom_filter_set_destroy",
@@ -72,6 +73,9 @@ def lib() -> ctypes.CDLL:
         "adl_bloom_build_segmented_device": (ctypes.c_int, [vp, vp, u32, vp, u32, i32, vp, vp, vp, u64, vp]),
         "adl_bloom_build": (ctypes.c_int, [vp, vp, u64, u32, i32, vp, vp]),
         "adl_bloom_build_segmented": (ctypes.c_int, [vp, vp, u32, vp, u32, i32, vp, vp, vp]),
+        "adl_bloom_filter_block_bytes": (u64, [vp, u32, i32]),
+        "adl_bloom_filter_block_workspace_bytes": (u64, [vp, u32, i32]),
+        "adl_bloom_filter_block_build_device": (ctypes.c_int, [vp, vp, u32, vp, u32, i32, vp, u64, vp, u64, vp]),
         "adl_bloom_probe_device": (ctypes.c_int, [vp, vp, u64, u32, i32, vp, u64, vp, vp]),
         "adl_bloom_probe_multi_device": (ctypes.c_int, [vp, vp, u64, u32, vp, u32, vp, vp, i32, vp, vp]),
         "adl_bloom_probe": (ctypes.c_int, [vp, vp, u64, u32, i32, vp, u64, vp, vp]),
@@ -233,6 +237,33 @@ def build_segmented(keys, key_begin, offsets=None, bits_per_key: int = 10, strea
                                                   _stream(stream)), "adl_bloom_build_segmented_device")
     torch.cuda.current_stream().synchronize()  # ws/out lifetimes end with this call's tensors
     return out, boff, sizes
+
+
+def filter_block_bytes(key_begin, bits_per_key: int = 10) -> int:
+    kb = np.ascontiguousarray(key_begin, dtype=np.uint64)
+    return lib().adl_bloom_filter_block_bytes(kb.ctypes.data, len(kb) - 1, bits_per_key)
+
+
+def build_filter_block(keys, key_begin, offsets=None, bits_per_key: int = 10, stream=None):
+    """FilterBlockWriter: Keys2Block() per filter + Final(), framed on the device
+    (adl_bloom_filter_block_build_device).  Returns the whole block as a uint8
+    device tensor, byte-identical to the reference's."""
+    kb = np.ascontiguousarray(key_begin, dtype=np.uint64)
+    F = len(kb) - 1
+    L = lib()
+    nbytes = L.adl_bloom_filter_block_bytes(kb.ctypes.data, F, bits_per_key)
+    if nbytes == 0:
+        raise AdlBloomError(-2, "filter block size")
+    ws_bytes = L.adl_bloom_filter_block_workspace_bytes(kb.ctypes.data, F, bits_per_key)
+    dev = keys.device if keys is not None else "cuda"
+    block = empty_device(nbytes, dev)
+    ws = empty_device(ws_bytes, dev)
+    stride = 0 if offsets is not None else (int(keys.shape[1]) if keys is not None else 16)
+    _check(L.adl_bloom_filter_block_build_device(_dptr(keys), _dptr(offsets), stride, kb.ctypes.data, F,
+                                                 bits_per_key, _dptr(block), nbytes, _dptr(ws), ws_bytes,
+                                                 _stream(stream)), "adl_bloom_filter_block_build_device")
+    _torch().cuda.current_stream().synchronize()  # ws lifetime ends with this call
+    return block[:nbytes]
 
 
 def _host_ptr(a):

@@ -78,6 +78,46 @@ RC BloomFilter::Keys2Block(const KeyArena &keys, string &result) {
   return OK;
 }
 
+RC FilterAlgorithm::Keys2Blocks(const KeyArena &keys, const vector<uint64_t> &key_begin, string &result,
+                                vector<uint64_t> &starts) {
+  starts.clear();
+  for (size_t f = 0; f + 1 < key_begin.size(); ++f) {
+    starts.push_back(result.size());
+    KeyArena part;
+    for (uint64_t i = key_begin[f]; i < key_begin[f + 1]; ++i)
+      part.Add(string_view(keys.bytes()).substr(keys.offsets()[i], keys.offsets()[i + 1] - keys.offsets()[i]));
+    if (RC rc = Keys2Block(part, result); rc != OK) return rc;
+  }
+  return OK;
+}
+
+/* All filters of a block in one pipelined segmented build, each bitmap written
+ * in place at the offset successive Keys2Block appends would give it. */
+RC BloomFilter::Keys2Blocks(const KeyArena &keys, const vector<uint64_t> &key_begin, string &result,
+                            vector<uint64_t> &off) {
+  const size_t nf = key_begin.size() - 1;
+  off.assign(nf, 0);
+  if (nf == 0) return OK;
+  const size_t init_len = result.size();
+  uint64_t total = 0;
+  for (size_t f = 0; f < nf; ++f) {
+    const uint64_t bytes = adl_bloom_bitmap_bytes(key_begin[f + 1] - key_begin[f], bits_per_key_);
+    if (bytes == 0) return OUT_OF_RANGE;
+    off[f] = init_len + total;
+    total += bytes;
+  }
+  result.resize(init_len + total);
+  const int st = adl_bloom_build_segmented(reinterpret_cast<const uint8_t *>(keys.bytes().data()),
+                                           keys.offsets().data(), 0, key_begin.data(), (uint32_t)nf,
+                                           bits_per_key_, reinterpret_cast<uint8_t *>(&result[0]), off.data(),
+                                           nullptr);
+  if (st != ADL_OK) {
+    result.resize(init_len);
+    return FromStatus(st);
+  }
+  return OK;
+}
+
 /* src/filter_block.cpp:49-62 -- one key against a host bitmap view.  The
  * bitmap is not resident, so this uploads it; FilterBlockReader keeps its
  * bitmaps on the device instead.  A device failure answers true ("may be
@@ -126,24 +166,30 @@ RC FilterBlockWriter::Update(string_view key) {
   return OK;
 }
 
-/* src/filter_block.cpp:104-109 -- one GPU build for the whole pending batch. */
+/* src/filter_block.cpp:104-109 -- closes the current filter; its bitmap is
+ * built with all the others in Final(). */
 RC FilterBlockWriter::Keys2Block() {
-  offsets_.push_back((int)buffer_.size());
-  RC rc = method_->Keys2Block(keys_, buffer_);
-  keys_.Clear();
-  if (rc != OK && status_ == OK) status_ = rc;
-  return rc;
+  bounds_.push_back(keys_.size());
+  return OK;
 }
 
 /* src/filter_block.cpp:77-102 -- [bitmaps][int32 offsets][int32 offsets_start]
  * [int32 num_filters][info]["int32 info_len"], moved out into `result`.
  * Returns the first Keys2Block failure (the reference cannot fail here). */
 RC FilterBlockWriter::Final(string &result) {
-  if (!keys_.empty()) Keys2Block();
+  if (keys_.size() > bounds_.back()) Keys2Block();
+  vector<uint64_t> offsets;
+  const RC rc = method_->Keys2Blocks(keys_, bounds_, buffer_, offsets);
+  keys_.Clear();
+  bounds_.assign(1, 0);
+  if (rc != OK) {
+    buffer_.clear();
+    return rc;
+  }
   const int offsets_start = (int)buffer_.size();
-  for (int off : offsets_) Append32(buffer_, off);
+  for (uint64_t off : offsets) Append32(buffer_, (int)off);
   Append32(buffer_, offsets_start);
-  Append32(buffer_, (int)offsets_.size());
+  Append32(buffer_, (int)offsets.size());
   string info;
   method_->FilterInfo(info);
   if (!info.empty()) {
@@ -152,10 +198,7 @@ RC FilterBlockWriter::Final(string &result) {
   }
   result = std::move(buffer_);
   buffer_.clear();
-  offsets_.clear();
-  RC rc = status_;
-  status_ = OK;
-  return rc;
+  return OK;
 }
 
 // ------------------------------------------------------------- FilterBlockReader

@@ -6,8 +6,10 @@
 // src/sstable.cpp and test/filter_block_test.cpp compile against it unchanged.
 // What differs underneath:
 //   * FilterBlockWriter keeps its pending keys in a packed arena (bytes +
-//     uint64 offsets) instead of vector<string>, and Keys2Block() hands the
-//     whole batch to one GPU build (adl_bloom_build).
+//     uint64 offsets) instead of vector<string>.  Keys2Block() closes a filter;
+//     Final() builds every filter of the block in one pipelined segmented GPU
+//     build (adl_bloom_build_segmented) straight into the block buffer, at the
+//     byte offsets the reference's successive appends would give them.
 //   * FilterBlockReader::Init uploads the block's bitmaps once into a
 //     device-resident filter set; IsKeyExists probes on the GPU.  Batched
 //     IsKeysExist() is the intended read path (one launch per batch).
@@ -58,6 +60,12 @@ class FilterAlgorithm {
   virtual void FilterInfo(string &/*info*/) { /* NOTHING */ }
   /* batched extensions */
   virtual RC Keys2Block(const KeyArena &keys, string &result) = 0;
+  /* Keys2Block for consecutive filters: filter f = keys [key_begin[f],
+   * key_begin[f+1]); the bitmaps are appended to result back to back, as
+   * successive Keys2Block calls would, filter f starting at starts[f].  The
+   * default loops over Keys2Block. */
+  virtual RC Keys2Blocks(const KeyArena &keys, const vector<uint64_t> &key_begin, string &result,
+                         vector<uint64_t> &starts);
   virtual RC IsKeysExist(const KeyArena &keys, string_view bitmap, vector<uint8_t> &out) = 0;
   virtual ~FilterAlgorithm() = default;
 };
@@ -70,6 +78,8 @@ class BloomFilter : public FilterAlgorithm {
   bool IsKeyExists(string_view key, string_view bitmap) override;
   void FilterInfo(string &info) override;
   RC Keys2Block(const KeyArena &keys, string &result) override;
+  RC Keys2Blocks(const KeyArena &keys, const vector<uint64_t> &key_begin, string &result,
+                 vector<uint64_t> &starts) override;
   RC IsKeysExist(const KeyArena &keys, string_view bitmap, vector<uint8_t> &out) override;
   int bits_per_key() const { return bits_per_key_; }
   int num_probes() const { return k_; }
@@ -89,11 +99,10 @@ class FilterBlockWriter {
   RC Keys2Block();
 
  private:
-  KeyArena keys_;
-  vector<int> offsets_;
+  KeyArena keys_;              /* keys of every filter not yet built */
+  vector<uint64_t> bounds_{0}; /* filter f = keys_ [bounds_[f], bounds_[f+1]) */
   string buffer_;
   unique_ptr<FilterAlgorithm> method_;
-  RC status_ = OK; /* first failure of a Keys2Block(), reported by Final() */
 };
 
 /* src/filter_block.hpp:54-73 */

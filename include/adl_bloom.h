@@ -118,6 +118,33 @@ int adl_bloom_build_segmented(const uint8_t *h_keys, const uint64_t *h_offsets, 
                               const uint64_t *key_begin, uint32_t num_filters, int32_t bits_per_key,
                               uint8_t *h_bitmaps, const uint64_t *h_bitmap_off, void *stream);
 
+/* ------------------------------------------------- filter block on the device */
+
+/* Size of the filter block FilterBlockWriter::Final (src/filter_block.cpp:77-102)
+ * writes for num_filters filters, filter f holding keys [key_begin[f],
+ * key_begin[f+1]) (HOST array, num_filters+1 entries): the bitmaps back to back
+ * (n_f*bpk+7 bytes each), then i32 offsets[F], i32 offsets_start, i32 F,
+ * "bf:" + i32 bpk, i32 7.  0 on invalid input or a block beyond the
+ * reference's int offsets. */
+uint64_t adl_bloom_filter_block_bytes(const uint64_t *key_begin, uint32_t num_filters,
+                                      int32_t bits_per_key);
+
+/* Workspace for adl_bloom_filter_block_build_device: the build workspace plus
+ * the 16-byte-aligned bitmaps before they are packed. */
+uint64_t adl_bloom_filter_block_workspace_bytes(const uint64_t *key_begin, uint32_t num_filters,
+                                                int32_t bits_per_key);
+
+/* Build num_filters filters from device-resident keys and frame them as one
+ * filter block in d_block (16-byte aligned, >= adl_bloom_filter_block_bytes):
+ * byte-identical to FilterBlockWriter::Keys2Block() per filter followed by
+ * Final() (src/filter_block.cpp:77-109), so one D2H -- or one direct file
+ * write -- emits the block.  num_filters == 0 gives the 19-byte empty block. */
+int adl_bloom_filter_block_build_device(const uint8_t *d_keys, const uint64_t *d_offsets,
+                                        uint32_t key_stride, const uint64_t *key_begin,
+                                        uint32_t num_filters, int32_t bits_per_key,
+                                        uint8_t *d_block, uint64_t block_bytes, void *d_workspace,
+                                        uint64_t workspace_bytes, void *stream);
+
 /* ---------------------------------------------------------------- probe */
 
 /* Probe n keys against one device bitmap of bitmap_bytes bytes (the exact
@@ -187,8 +214,9 @@ int adl_bloom_murmur3(uint32_t seed, const void *data, uint64_t len, uint32_t *h
 /* ---------------------------------------------------------------- instrumentation */
 
 /* Per-kernel timing of the build for the calling thread: while enabled, each
- * build records HIP events on its stream around pass A (bloom_bin_kernel) and
- * pass B (bloom_tile_kernel); up to `capacity` builds are kept.  collect()
+ * build takes start/stop timestamps of pass A (bloom_bin_kernel) and pass B
+ * (bloom_tile_kernel) from their dispatch packets (hipExtLaunchKernel events,
+ * nothing extra enqueued between the launches); up to `capacity` builds are kept.  collect()
  * synchronises on the recorded events, writes the summed milliseconds of the
  * two kernels to ms[0] (pass A) and ms[1] (pass B), the number of timed builds
  * to *builds, and disables timing.  Used by bench.py for the live roofline. */

@@ -481,3 +481,47 @@ def test_errors_are_status_codes(dev, ab):
                                     1 << 20, st) == -2
     assert L.adl_bloom_build_device(keys.data_ptr(), None, 16, 16, 10, out.data_ptr() + 1, ws.data_ptr(),
                                     1 << 20, st) == -1  # misaligned bitmap
+
+
+# ------------------------------------------------ filter block framed on the device (§8f rank 3)
+def test_filter_block_device_reference_scenario(dev, ab, golden, oracle):
+    """test/filter_block_test.cpp:7-31 -- two Keys2Block() calls then Final(),
+    emitted as one device buffer: the reference block's SHA-256."""
+    b0 = [b"hello", b"world", b"hello-yly", b"hello-ddl"] + [b"hello-ddl%d" % i for i in range(10000)]
+    b1 = [b"adl", b"dont", b"like-apple"]
+    dk, do, _, _ = packed_dev(dev, b0 + b1)
+    blk = ab.build_filter_block(dk, [0, len(b0), len(b0) + len(b1)], offsets=do)
+    raw = blk.cpu().numpy().tobytes()
+    g = golden["appendix_b"]["filter_block_test"]
+    assert len(raw) == g["bytes"]
+    assert hashlib.sha256(raw).hexdigest() == g["sha256"]
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_filter_block_device_many_filters(dev, ab, oracle, seed):
+    """>64 filters (several pack launches), tiny 7- and 17-byte bitmaps side by
+    side (one 16-byte word meets up to 4 of them), empty filters, larger ones."""
+    rng = np.random.default_rng(seed)
+    sizes = list(rng.choice([0, 1, 2, 3, 5, 17, 100, 1000, 6001], size=150))
+    sizes[70:74] = [0, 0, 1, 0]
+    sizes.append(120_000)
+    kb = np.concatenate([[0], np.cumsum(sizes)]).astype(np.uint64)
+    keys = oracle.splitmix_keys16(0x5EED + seed, int(kb[-1]))
+    blk = ab.build_filter_block(dev.from_numpy(keys).cuda(), kb)
+    bms = [oracle.keys2block(keys[int(kb[f]):int(kb[f + 1])]) for f in range(len(sizes))]
+    want = oracle.filter_block_final([b.tobytes() for b in bms], 10)
+    got = blk.cpu().numpy().tobytes()
+    assert len(got) == len(want) == ab.filter_block_bytes(kb)
+    assert got == want
+
+
+def test_filter_block_device_empty_and_bpk(dev, ab, oracle):
+    kb0 = np.array([0], dtype=np.uint64)
+    blk = ab.build_filter_block(None, kb0)
+    assert blk.cpu().numpy().tobytes() == oracle.filter_block_final([], 10)
+    keys = oracle.splitmix_keys16(9, 3000)
+    for bpk in (1, 7, 23):
+        kb = np.array([0, 1000, 1000, 3000], dtype=np.uint64)
+        blk = ab.build_filter_block(dev.from_numpy(keys).cuda(), kb, bits_per_key=bpk)
+        bms = [oracle.keys2block(keys[int(kb[f]):int(kb[f + 1])], bits_per_key=bpk).tobytes() for f in range(3)]
+        assert blk.cpu().numpy().tobytes() == oracle.filter_block_final(bms, bpk)
