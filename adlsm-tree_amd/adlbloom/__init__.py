@@ -34,7 +34,10 @@ EXPORTS = (
     "adl_bloom_bitmap_bytes", "adl_bloom_bitmap_alloc_bytes", "adl_bloom_build_workspace_bytes",
     "adl_bloom_build_device", "adl_bloom_build_segmented_device", "adl_bloom_build",
     "adl_bloom_build_segmented", "adl_bloom_filter_block_bytes", "adl_bloom_filter_block_workspace_bytes",
-    "adl_bloom_filter_block_build_device",
+    "adl_bloom_filter_block_build_device", "adl_bloom_probe_ranges_device",
+    "adl_bloom_filter_cache_create", "adl_bloom_filter_cache_destroy", "adl_bloom_filter_cache_put",
+    "adl_bloom_filter_cache_contains", "adl_bloom_filter_cache_remove", "adl_bloom_filter_cache_stats",
+    "adl_bloom_filter_cache_probe",
     "adl_bloom_probe_device", "adl_bloom_probe_multi_device", "adl_bloom_probe",
     "adl_bloom_filter_set_create", "adl_bloom_filter_set_probe",
     "adl_bloom_filter_set_device_view", "adl_bloom_filter_set_destroy",
@@ -76,6 +79,15 @@ def lib() -> ctypes.CDLL:
         "adl_bloom_filter_block_bytes": (u64, [vp, u32, i32]),
         "adl_bloom_filter_block_workspace_bytes": (u64, [vp, u32, i32]),
         "adl_bloom_filter_block_build_device": (ctypes.c_int, [vp, vp, u32, vp, u32, i32, vp, u64, vp, u64, vp]),
+        "adl_bloom_probe_ranges_device": (ctypes.c_int, [vp, vp, u64, u32, vp, u32, vp, vp, vp, i32, vp, vp]),
+        "adl_bloom_filter_cache_create": (ctypes.c_int, [u64, u32, i32, ctypes.POINTER(vp)]),
+        "adl_bloom_filter_cache_destroy": (ctypes.c_int, [vp]),
+        "adl_bloom_filter_cache_put": (ctypes.c_int, [vp, ctypes.c_char_p, u64, vp, u64]),
+        "adl_bloom_filter_cache_contains": (ctypes.c_int, [vp, ctypes.c_char_p, u64]),
+        "adl_bloom_filter_cache_remove": (ctypes.c_int, [vp, ctypes.c_char_p, u64]),
+        "adl_bloom_filter_cache_stats": (ctypes.c_int, [vp, ctypes.POINTER(u32), ctypes.POINTER(u64)]),
+        "adl_bloom_filter_cache_probe": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_char_p), vp, u32, u32, vp, vp,
+                                                         u64, u32, vp, vp, ctypes.POINTER(u64), vp]),
         "adl_bloom_probe_device": (ctypes.c_int, [vp, vp, u64, u32, i32, vp, u64, vp, vp]),
         "adl_bloom_probe_multi_device": (ctypes.c_int, [vp, vp, u64, u32, vp, u32, vp, vp, i32, vp, vp]),
         "adl_bloom_probe": (ctypes.c_int, [vp, vp, u64, u32, i32, vp, u64, vp, vp]),
@@ -399,6 +411,65 @@ class FilterSet:
     def close(self):
         if self._h:
             lib().adl_bloom_filter_set_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class FilterCache:
+    """Device-resident filter blocks keyed by SSTable oid, LRU (adl_bloom_filter_cache)."""
+
+    def __init__(self, capacity_bytes: int, max_tables: int = 64, bits_per_key: int = 10):
+        self._h = ctypes.c_void_p()
+        _check(lib().adl_bloom_filter_cache_create(capacity_bytes, max_tables, bits_per_key, ctypes.byref(self._h)),
+               "adl_bloom_filter_cache_create")
+
+    def put(self, oid: bytes, block: bytes) -> None:
+        b = np.frombuffer(block, dtype=np.uint8)
+        _check(lib().adl_bloom_filter_cache_put(self._h, oid, len(oid), b.ctypes.data, b.size),
+               "adl_bloom_filter_cache_put")
+
+    def put_status(self, oid: bytes, block: bytes) -> int:
+        b = np.frombuffer(block, dtype=np.uint8)
+        return lib().adl_bloom_filter_cache_put(self._h, oid, len(oid), b.ctypes.data, b.size)
+
+    def __contains__(self, oid: bytes) -> bool:
+        return lib().adl_bloom_filter_cache_contains(self._h, oid, len(oid)) == 1
+
+    def remove(self, oid: bytes) -> bool:
+        return lib().adl_bloom_filter_cache_remove(self._h, oid, len(oid)) == 1
+
+    def stats(self):
+        t, b = ctypes.c_uint32(), ctypes.c_uint64()
+        _check(lib().adl_bloom_filter_cache_stats(self._h, ctypes.byref(t), ctypes.byref(b)), "stats")
+        return t.value, b.value
+
+    def probe(self, oids, table, keys: np.ndarray, offsets=None, filter: int = 0):
+        """Query i against filter `filter` of table oids[table[i]]; returns (0/1 array, uncached count)."""
+        keys = np.ascontiguousarray(keys, dtype=np.uint8)
+        if offsets is None:
+            n, stride, po = keys.shape[0], keys.shape[1], None
+        else:
+            offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+            n, stride, po = len(offsets) - 1, 0, offsets.ctypes.data
+        arr = (ctypes.c_char_p * max(len(oids), 1))(*oids)
+        lens = np.array([len(o) for o in oids] or [0], dtype=np.uint64)
+        tab = np.ascontiguousarray(table, dtype=np.uint32)
+        out = np.empty(max(n, 1), dtype=np.uint8)
+        unc = ctypes.c_uint64()
+        _check(lib().adl_bloom_filter_cache_probe(self._h, arr, lens.ctypes.data, len(oids), filter,
+                                                  keys.ctypes.data, po, n, stride, tab.ctypes.data,
+                                                  out.ctypes.data, ctypes.byref(unc), None),
+               "adl_bloom_filter_cache_probe")
+        return out[:n], unc.value
+
+    def close(self):
+        if self._h:
+            lib().adl_bloom_filter_cache_destroy(self._h)
             self._h = ctypes.c_void_p()
 
     def __del__(self):

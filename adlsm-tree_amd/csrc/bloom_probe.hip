@@ -82,12 +82,13 @@ template <class Keys>
 __global__ __launch_bounds__(kBlockP) void bloom_probe_multi_kernel(
     Keys keys, uint64_t n, uint32_t k, ProbeGroups pg, const uint32_t *__restrict__ fid, uint32_t uniform_f,
     uint32_t nf, const uint8_t *__restrict__ bitmaps, const uint64_t *__restrict__ boff,
-    uint8_t *__restrict__ out) {
+    const uint64_t *__restrict__ bend, uint8_t *__restrict__ out) {
+  // filter f = bitmaps[boff[f], bend[f]), or [boff[f], boff[f+1]) when bend is null
   extern __shared__ ModLds lmod[];
   const bool lds_tab = nf <= kLdsFilters;
   if (lds_tab) {
     for (uint32_t f = threadIdx.x; f < nf; f += kBlockP) {
-      const FastMod fm = fastmod_for((uint32_t)((boff[f + 1] - boff[f]) * 8));
+      const FastMod fm = fastmod_for((uint32_t)(((bend ? bend[f] : boff[f + 1]) - boff[f]) * 8));
       lmod[f] = ModLds{fm.magic, fm.shift};
     }
     __syncthreads();
@@ -97,7 +98,7 @@ __global__ __launch_bounds__(kBlockP) void bloom_probe_multi_kernel(
     const uint32_t f = fid ? fid[i] : uniform_f;  // fid == nullptr: every query -> uniform_f
     uint8_t hit = 0;
     if (f < nf) {
-      const uint64_t b0 = boff[f], b1 = boff[f + 1];
+      const uint64_t b0 = boff[f], b1 = bend ? bend[f] : boff[f + 1];
       const uint32_t m = (uint32_t)((b1 - b0) * 8);
       if (m != 0) {
         FastMod mod;
@@ -275,7 +276,7 @@ namespace {
 int probe_multi(const uint8_t *d_keys, const uint64_t *d_offsets, uint64_t n, uint32_t key_stride,
                 const uint32_t *d_filter_id, uint32_t uniform_f, uint32_t num_filters,
                 const uint8_t *d_bitmaps, const uint64_t *d_bitmap_off, int32_t bits_per_key,
-                uint8_t *d_out, hipStream_t st) {
+                uint8_t *d_out, hipStream_t st, const uint64_t *d_bitmap_end = nullptr) {
   if (num_filters && (!d_bitmaps || !d_bitmap_off)) return ADL_ERR_INVALID_ARG;
   if (!d_offsets && key_stride == 0) return ADL_ERR_INVALID_ARG;
   const uint32_t k = (uint32_t)adl_host::num_probes(bits_per_key);
@@ -283,12 +284,24 @@ int probe_multi(const uint8_t *d_keys, const uint64_t *d_offsets, uint64_t n, ui
     const size_t lds = num_filters <= kLdsFilters ? (size_t)num_filters * sizeof(ModLds) : 0;
     hipLaunchKernelGGL(bloom_probe_multi_kernel<decltype(keys)>, dim3(grid_for(n, kBlockP, 8)),
                        dim3(kBlockP), lds, st, keys, n, k, probe_groups(), d_filter_id, uniform_f, num_filters,
-                       d_bitmaps, d_bitmap_off, d_out);
+                       d_bitmaps, d_bitmap_off, d_bitmap_end, d_out);
     ADL_HIP_TRY(hipGetLastError());
     return ADL_OK;
   });
 }
 }  // namespace
+
+extern "C" int adl_bloom_probe_ranges_device(const uint8_t *d_keys, const uint64_t *d_offsets, uint64_t n,
+                                             uint32_t key_stride, const uint32_t *d_filter_id,
+                                             uint32_t num_filters, const uint8_t *d_bitmaps,
+                                             const uint64_t *d_begin, const uint64_t *d_end,
+                                             int32_t bits_per_key, uint8_t *d_out, void *stream) {
+  if (n == 0) return ADL_OK;
+  if (!d_keys || !d_filter_id || !d_out || bits_per_key < 0) return ADL_ERR_INVALID_ARG;
+  if (num_filters && !d_end) return ADL_ERR_INVALID_ARG;
+  return probe_multi(d_keys, d_offsets, n, key_stride, d_filter_id, 0, num_filters, d_bitmaps, d_begin,
+                     bits_per_key, d_out, (hipStream_t)stream, d_end);
+}
 
 extern "C" {
 

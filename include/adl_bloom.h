@@ -165,6 +165,15 @@ int adl_bloom_probe_multi_device(const uint8_t *d_keys, const uint64_t *d_offset
                                  const uint64_t *d_bitmap_off, int32_t bits_per_key,
                                  uint8_t *d_out, void *stream);
 
+/* Like adl_bloom_probe_multi_device, with filter f = d_bitmaps[d_begin[f] ..
+ * d_end[f]) (device arrays, num_filters entries each): the filters may sit
+ * anywhere in one device arena, in any order (adl_bloom_filter_cache). */
+int adl_bloom_probe_ranges_device(const uint8_t *d_keys, const uint64_t *d_offsets, uint64_t n,
+                                  uint32_t key_stride, const uint32_t *d_filter_id,
+                                  uint32_t num_filters, const uint8_t *d_bitmaps,
+                                  const uint64_t *d_begin, const uint64_t *d_end,
+                                  int32_t bits_per_key, uint8_t *d_out, void *stream);
+
 /* Host-pointer convenience for adl_bloom_probe_device.  Synchronous. */
 int adl_bloom_probe(const uint8_t *h_keys, const uint64_t *h_offsets, uint64_t n,
                     uint32_t key_stride, int32_t bits_per_key, const uint8_t *h_bitmap,
@@ -198,6 +207,48 @@ int adl_bloom_filter_set_device_view(const adl_bloom_filter_set *set, const uint
                                      const uint64_t **d_bitmap_off, uint32_t *num_filters);
 
 int adl_bloom_filter_set_destroy(adl_bloom_filter_set *set);
+
+/* ------------------------------------------- filter cache keyed by SSTable oid */
+
+/* Device-resident filter blocks of many SSTables in one arena of
+ * capacity_bytes, keyed by oid (any byte string, e.g. the SHA-256 file name),
+ * least recently used evicted first, at most max_tables blocks: the filter
+ * side of DB::table_cache_ (src/db.hpp:96-97, LRUCache src/cache.hpp:23-93).
+ * Every block must carry bits_per_key.  Thread-safe (one mutex per cache). */
+typedef struct adl_bloom_filter_cache adl_bloom_filter_cache;
+
+int adl_bloom_filter_cache_create(uint64_t capacity_bytes, uint32_t max_tables, int32_t bits_per_key,
+                                  adl_bloom_filter_cache **out);
+int adl_bloom_filter_cache_destroy(adl_bloom_filter_cache *cache);
+
+/* Insert (or replace) the filter block of table `oid`: validated as
+ * FilterBlockReader::Init does (ADL_FILTER_BLOCK_ERROR), ADL_ERR_INVALID_ARG if
+ * its bits_per_key differs from the cache's; its bitmaps are uploaded once
+ * and it becomes the most recently used.  Synchronous. */
+int adl_bloom_filter_cache_put(adl_bloom_filter_cache *cache, const char *oid, uint64_t oid_len,
+                               const uint8_t *h_block, uint64_t block_len);
+
+/* 1 if cached (and now most recently used), else 0. */
+int adl_bloom_filter_cache_contains(adl_bloom_filter_cache *cache, const char *oid, uint64_t oid_len);
+
+/* 1 if removed, 0 if it was not cached. */
+int adl_bloom_filter_cache_remove(adl_bloom_filter_cache *cache, const char *oid, uint64_t oid_len);
+
+int adl_bloom_filter_cache_stats(adl_bloom_filter_cache *cache, uint32_t *tables, uint64_t *bytes_used);
+
+/* Multi-get: query i (host keys) probes filter `filter` (0 for SSTables) of
+ * table h_table[i], an index into the oid list oids[0..num_tables).  One
+ * launch for the batch.  A query bound for a table that is not cached
+ * answers 1 ("may be present": read the table); one bound for a filter the
+ * block does not have answers 0 (src/filter_block.cpp:174).  *h_uncached
+ * (optional) counts the queries whose table was not cached.  Synchronous.
+ * Replaces SSTableReader::Get's filter check (src/sstable.cpp:238) across the
+ * tables of a multi-get. */
+int adl_bloom_filter_cache_probe(adl_bloom_filter_cache *cache, const char *const *oids,
+                                 const uint64_t *oid_lens, uint32_t num_tables, uint32_t filter,
+                                 const uint8_t *h_keys, const uint64_t *h_offsets, uint64_t n,
+                                 uint32_t key_stride, const uint32_t *h_table, uint8_t *h_out,
+                                 uint64_t *h_uncached, void *stream);
 
 /* ---------------------------------------------------------------- hash */
 

@@ -525,3 +525,77 @@ def test_filter_block_device_empty_and_bpk(dev, ab, oracle):
         blk = ab.build_filter_block(dev.from_numpy(keys).cuda(), kb, bits_per_key=bpk)
         bms = [oracle.keys2block(keys[int(kb[f]):int(kb[f + 1])], bits_per_key=bpk).tobytes() for f in range(3)]
         assert blk.cpu().numpy().tobytes() == oracle.filter_block_final(bms, bpk)
+
+
+# ------------------------------------------------ filter cache keyed by SSTable oid (§8f rank 2)
+def _table_block(oracle, seed, n, bpk=10):
+    keys = oracle.splitmix_keys16(seed, n)
+    return keys, oracle.filter_block_final([oracle.keys2block(keys, bits_per_key=bpk).tobytes()], bpk)
+
+
+def test_filter_cache_multiget(dev, ab, oracle):
+    """Many SSTables' blocks in one device arena; one multi-get batch over
+    cached and uncached tables, every answer against the oracle."""
+    sizes = [1000, 5000, 0, 20000, 333, 70000, 1, 4096]
+    tables = [_table_block(oracle, 100 + t, n) for t, n in enumerate(sizes)]
+    oids = [b"%064x" % (0xABC0 + t) for t in range(len(sizes))]
+    cache = ab.FilterCache(64 << 20, max_tables=64)
+    for t in range(len(sizes) - 1):  # the last table stays uncached
+        cache.put(oids[t], tables[t][1])
+    assert cache.stats()[0] == len(sizes) - 1
+    rng = np.random.default_rng(5)
+    nq = 50000
+    table = rng.integers(0, len(sizes), nq).astype(np.uint32)
+    q = oracle.splitmix_keys16(0xFEED, nq)
+    for i in range(0, nq, 3):  # a third of the queries are inserted keys of their table
+        keys = tables[table[i]][0]
+        if len(keys):
+            q[i] = keys[rng.integers(0, len(keys))]
+    got, unc = cache.probe(oids, table, q)
+    want = np.ones(nq, dtype=np.uint8)
+    for t in range(len(sizes) - 1):
+        sel = table == t
+        bm = oracle.keys2block(tables[t][0])
+        want[sel] = oracle.probe(q[sel], bm)
+    assert np.array_equal(got, want)
+    assert unc == int((table == len(sizes) - 1).sum())
+    # a filter index the blocks do not have answers 0
+    got1, _ = cache.probe(oids[:1], np.zeros(10, np.uint32), q[:10], filter=1)
+    assert not got1.any()
+    cache.close()
+
+
+def test_filter_cache_lru_and_errors(dev, ab, oracle):
+    blocks = [_table_block(oracle, 7 + t, 20000)[1] for t in range(6)]  # ~200 KB bitmaps each
+    cache = ab.FilterCache(3 * 201 * 1024, max_tables=64)  # room for 3 blocks
+    for t in range(3):
+        cache.put(b"t%d" % t, blocks[t])
+    assert b"t0" in cache  # t0 becomes most recently used: t1 is now the LRU
+    cache.put(b"t3", blocks[3])
+    assert b"t1" not in cache and b"t0" in cache and b"t2" in cache and b"t3" in cache
+    assert cache.remove(b"t2") and not cache.remove(b"t2")
+    cache.put(b"t4", blocks[4])
+    assert cache.stats()[0] == 3
+    # max_tables, as LRUCache's maxSize
+    small = ab.FilterCache(16 << 20, max_tables=2)
+    for t in range(3):
+        small.put(b"s%d" % t, blocks[t])
+    assert small.stats()[0] == 2 and b"s0" not in small
+    # FilterBlockReader::Init's errors; a block of another bits_per_key
+    assert cache.put_status(b"bad", b"\x00\x01") == ab.ADL_FILTER_BLOCK_ERROR
+    assert cache.put_status(b"bad", blocks[0][:-3]) == ab.ADL_FILTER_BLOCK_ERROR
+    other = oracle.filter_block_final([oracle.keys2block(oracle.splitmix_keys16(1, 100), bits_per_key=12).tobytes()], 12)
+    assert cache.put_status(b"bpk", other) == -1
+    # the reference test scenario's block: both filters probed through the cache
+    b0 = [b"hello", b"world", b"hello-yly", b"hello-ddl"] + [b"hello-ddl%d" % i for i in range(10000)]
+    b1 = [b"adl", b"dont", b"like-apple"]
+    blk = oracle.filter_block_final([oracle.keys2block(b0).tobytes(), oracle.keys2block(b1).tobytes()], 10)
+    cache.put(b"fbt", blk)
+    d0, o0 = oracle.pack(b0)
+    got, _ = cache.probe([b"fbt"], np.zeros(len(b0), np.uint32), d0, offsets=o0, filter=0)
+    assert got.all()
+    d1, o1 = oracle.pack(b1)
+    got, _ = cache.probe([b"fbt"], np.zeros(len(b1), np.uint32), d1, offsets=o1, filter=1)
+    assert got.all()
+    small.close()
+    cache.close()
