@@ -34,7 +34,7 @@ EXPORTS = (
     "adl_bloom_bitmap_bytes", "adl_bloom_bitmap_alloc_bytes", "adl_bloom_build_workspace_bytes",
     "adl_bloom_build_device", "adl_bloom_build_segmented_device", "adl_bloom_build",
     "adl_bloom_build_segmented", "adl_bloom_filter_block_bytes", "adl_bloom_filter_block_workspace_bytes",
-    "adl_bloom_filter_block_build_device", "adl_bloom_probe_ranges_device",
+    "adl_bloom_filter_block_build_device", "adl_bloom_probe_ranges_device", "adl_bloom_build_segmented_device_ex",
     "adl_bloom_filter_cache_create", "adl_bloom_filter_cache_destroy", "adl_bloom_filter_cache_put",
     "adl_bloom_filter_cache_contains", "adl_bloom_filter_cache_remove", "adl_bloom_filter_cache_stats",
     "adl_bloom_filter_cache_probe",
@@ -79,6 +79,7 @@ def lib() -> ctypes.CDLL:
         "adl_bloom_filter_block_bytes": (u64, [vp, u32, i32]),
         "adl_bloom_filter_block_workspace_bytes": (u64, [vp, u32, i32]),
         "adl_bloom_filter_block_build_device": (ctypes.c_int, [vp, vp, u32, vp, u32, i32, vp, u64, vp, u64, vp]),
+        "adl_bloom_build_segmented_device_ex": (ctypes.c_int, [vp, vp, u32, vp, u32, i32, vp, vp, u32, vp, u64, vp]),
         "adl_bloom_probe_ranges_device": (ctypes.c_int, [vp, vp, u64, u32, vp, u32, vp, vp, vp, i32, vp, vp]),
         "adl_bloom_filter_cache_create": (ctypes.c_int, [u64, u32, i32, ctypes.POINTER(vp)]),
         "adl_bloom_filter_cache_destroy": (ctypes.c_int, [vp]),
@@ -226,7 +227,10 @@ def build(keys, offsets=None, bits_per_key: int = 10, stream=None):
     return Builder(n, bits_per_key, keys.device).build(keys, offsets, stream)
 
 
-def build_segmented(keys, key_begin, offsets=None, bits_per_key: int = 10, stream=None):
+SKIP_ADJACENT_DUPLICATES = 1
+
+
+def build_segmented(keys, key_begin, offsets=None, bits_per_key: int = 10, stream=None, flags: int = 0):
     """Many independent filters in one pass pair.  key_begin: host ints (F+1).
     Returns (device bitmaps buffer, host bitmap byte offsets (F), exact sizes (F))."""
     torch = _torch()
@@ -244,9 +248,9 @@ def build_segmented(keys, key_begin, offsets=None, bits_per_key: int = 10, strea
     pk = _dptr(keys)
     po = _dptr(offsets)
     stride = 0 if offsets is not None else keys.shape[1]
-    _check(lib().adl_bloom_build_segmented_device(pk, po, stride, kb.ctypes.data, F, bits_per_key,
-                                                  _dptr(out), boff.ctypes.data, _dptr(ws), ws_bytes,
-                                                  _stream(stream)), "adl_bloom_build_segmented_device")
+    _check(lib().adl_bloom_build_segmented_device_ex(pk, po, stride, kb.ctypes.data, F, bits_per_key,
+                                                     _dptr(out), boff.ctypes.data, flags, _dptr(ws), ws_bytes,
+                                                     _stream(stream)), "adl_bloom_build_segmented_device_ex")
     torch.cuda.current_stream().synchronize()  # ws/out lifetimes end with this call's tensors
     return out, boff, sizes
 

@@ -79,6 +79,7 @@ struct BuildArgs {
   uint32_t nt_bitmap;  // pass B: non-temporal bitmap stores (tuning, ADL_BLOOM_NT_BITMAP)
   uint32_t dyn_tiles;  // pass B: tiles from a work queue that pass A resets (ADL_BLOOM_DYN_TILES)
   uint32_t stage_keys; // pass A: LDS-staged variable-length keys (16-B aligned key buffer; ADL_BLOOM_STAGE_KEYS)
+  uint32_t dedup;      // skip a key equal to its predecessor in the same filter (ADL_BLOOM_SKIP_ADJACENT_DUPLICATES)
   uint32_t exp;        // diagnostics build only (ADL_BLOOM_EXP bits, wrong results): 1 no hash, 2 no stores
   FilterDesc f[kMaxFilters];
 };
@@ -330,13 +331,24 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin_kernel(BuildArgs a, Keys keys
         }
       }
     }
+    // live slots: valid, and (dedup) not equal to the previous key of the
+    // filter -- a repeated key sets the same bits, so skipping it leaves the
+    // bitmap unchanged (src/keys.cpp:61-74 feeds versions of a user key in a row)
+    uint32_t live = 0;
+#pragma unroll
+    for (int i = 0; i < KPT; ++i) {
+      if (slot_pos(i) < cnt) {
+        const uint32_t ki = first + kidx[i];
+        if (!(a.dedup && ki > 0 && keys.same_as_prev(d.key_begin + ki))) live |= 1u << i;
+      }
+    }
     __syncthreads();  // hist cleared (previous iteration / prologue); staging area free
 
     constexpr int KR = KFIX > 0 ? KFIX : 1;
     uint32_t pos[KPT][KR];
 #pragma unroll
     for (int i = 0; i < KPT; ++i) {
-      if (slot_pos(i) < cnt) {
+      if (live & (1u << i)) {
         if constexpr (KFIX > 0) {
 #pragma unroll
           for (int j = 0; j < KFIX; ++j) {
@@ -353,8 +365,8 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin_kernel(BuildArgs a, Keys keys
     }
     __syncthreads();
 
-    // Exclusive scan: hist[t] = start of tile t's run; hist[T] = k*cnt.
-    block_excl_scan_array<BLOCK>(hist, T + 1, scratch);
+    // Exclusive scan: hist[t] = start of tile t's run; hist[T] = k * live keys.
+    const uint32_t total = block_excl_scan_array<BLOCK>(hist, T + 1, scratch);
 
     // (tile, chunk) table, T+1 rows of W entries: row t = start of tile t.
     uint32_t *tab = table_ws + d.table_base;
@@ -364,7 +376,7 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin_kernel(BuildArgs a, Keys keys
     // Scatter tile offsets into LDS by tile (hist now serves as the cursor).
 #pragma unroll
     for (int i = 0; i < KPT; ++i) {
-      if (slot_pos(i) < cnt) {
+      if (live & (1u << i)) {
         if constexpr (KFIX > 0) {
           // all k cursor bumps in flight before the first dependent write
           uint32_t slot_l[KFIX];
@@ -386,7 +398,6 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin_kernel(BuildArgs a, Keys keys
     // Stream the sorted chunk out to region w (a.cap positions, 16-byte
     // aligned).  The hist is cleared for the next chunk meanwhile.
     for (uint32_t i = tid; i <= T; i += BLOCK) hist[i] = 0;
-    const uint32_t total = k * cnt;
     uint32_t *dst = pos_ws + d.pos_base + (uint64_t)w * a.cap;
     const uint32_t nvec = total >> 2;
     const uint4 *src4 = reinterpret_cast<const uint4 *>(lpos);
@@ -962,7 +973,7 @@ int launch_binned(const Plan &p, Keys keys, uint8_t *d_bitmaps, void *ws, hipStr
     auto by_block = [&](auto k6, auto kgen) -> int {  // k6/kgen: tag types carrying BLOCK
       constexpr int B = decltype(k6)::value;
       if constexpr (std::is_same<Keys, Keys16>::value) {
-        if (p.a.k == 6 && !p.sequential_a) return go(bloom_bin16_kernel<B, 6>);
+        if (p.a.k == 6 && !p.sequential_a && !p.a.dedup) return go(bloom_bin16_kernel<B, 6>);
       }
       if (p.a.k == 6) return go(bloom_bin_kernel<B, 6, 6, Keys>);
       return go(bloom_bin_kernel<B, 0, kKptMax, Keys>);
@@ -1016,7 +1027,8 @@ namespace {
 int build_groups(const uint8_t *d_keys, const uint64_t *d_offsets, uint32_t key_stride,
                  const uint64_t *key_begin, uint32_t num_filters, int32_t bpk, uint8_t *d_bitmaps,
                  const uint64_t *bitmap_off, void *d_workspace, uint64_t workspace_bytes,
-                 hipStream_t st) {
+                 hipStream_t st, uint32_t flags = 0) {
+  if (flags & ~(uint32_t)ADL_BLOOM_SKIP_ADJACENT_DUPLICATES) return ADL_ERR_INVALID_ARG;
   if (!d_keys && key_begin[num_filters] > key_begin[0]) return ADL_ERR_INVALID_ARG;
   if (!d_offsets && key_stride == 0 && key_begin[num_filters] > key_begin[0]) return ADL_ERR_INVALID_ARG;
   const bool atomic = use_atomic_path();
@@ -1030,6 +1042,7 @@ int build_groups(const uint8_t *d_keys, const uint64_t *d_offsets, uint32_t key_
     Plan p;
     int rc = make_plan(counts, nf, bpk, p);
     if (rc) return rc;
+    p.a.dedup = (flags & ADL_BLOOM_SKIP_ADJACENT_DUPLICATES) ? 1u : 0u;
     for (uint32_t f = 0; f < nf; ++f) {
       if (bitmap_off[g + f] % 16) return ADL_ERR_INVALID_ARG;
       p.a.f[f].key_begin = key_begin[g + f];
@@ -1132,6 +1145,21 @@ int adl_bloom_build_segmented_device(const uint8_t *d_keys, const uint64_t *d_of
     if (reinterpret_cast<uintptr_t>(d_bitmaps) % 16) return ADL_ERR_INVALID_ARG;
     return build_groups(d_keys, d_offsets, key_stride, key_begin, num_filters, bits_per_key,
                         d_bitmaps, bitmap_off, d_workspace, workspace_bytes, (hipStream_t)stream);
+  } catch (...) {
+    return ADL_ERR_DEVICE;
+  }
+}
+
+int adl_bloom_build_segmented_device_ex(const uint8_t *d_keys, const uint64_t *d_offsets,
+                                        uint32_t key_stride, const uint64_t *key_begin,
+                                        uint32_t num_filters, int32_t bits_per_key,
+                                        uint8_t *d_bitmaps, const uint64_t *bitmap_off, uint32_t flags,
+                                        void *d_workspace, uint64_t workspace_bytes, void *stream) {
+  try {
+    if (!key_begin || !bitmap_off || !d_bitmaps || num_filters == 0) return ADL_ERR_INVALID_ARG;
+    if (reinterpret_cast<uintptr_t>(d_bitmaps) % 16) return ADL_ERR_INVALID_ARG;
+    return build_groups(d_keys, d_offsets, key_stride, key_begin, num_filters, bits_per_key,
+                        d_bitmaps, bitmap_off, d_workspace, workspace_bytes, (hipStream_t)stream, flags);
   } catch (...) {
     return ADL_ERR_DEVICE;
   }

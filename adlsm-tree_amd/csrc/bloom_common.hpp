@@ -29,6 +29,11 @@ struct Keys16 {
   __device__ __forceinline__ void hash(uint64_t i, uint32_t &h1, uint32_t &h2) const {
     hash16(keys[i], h1, h2);
   }
+  // key i == key i-1 (i > 0)
+  __device__ __forceinline__ bool same_as_prev(uint64_t i) const {
+    const uint4 a = keys[i], b = keys[i - 1];
+    return a.x == b.x && a.y == b.y && a.z == b.z && a.w == b.w;
+  }
 };
 
 // Fixed stride (any stride, any alignment).
@@ -37,6 +42,12 @@ struct KeysStride {
   uint32_t stride;
   __device__ __forceinline__ void hash(uint64_t i, uint32_t &h1, uint32_t &h2) const {
     hash_bytes(keys + i * stride, stride, kSeed1, kSeed2, h1, h2);
+  }
+  __device__ __forceinline__ bool same_as_prev(uint64_t i) const {
+    const uint8_t *a = keys + i * stride, *b = a - stride;
+    for (uint32_t j = 0; j < stride; ++j)
+      if (a[j] != b[j]) return false;
+    return true;
   }
 };
 
@@ -47,6 +58,13 @@ struct KeysVar {
   __device__ __forceinline__ void hash(uint64_t i, uint32_t &h1, uint32_t &h2) const {
     const uint64_t o0 = offs[i], o1 = offs[i + 1];
     hash_bytes(keys + o0, (uint32_t)(o1 - o0), kSeed1, kSeed2, h1, h2);
+  }
+  __device__ __forceinline__ bool same_as_prev(uint64_t i) const {
+    const uint64_t p0 = offs[i - 1], o0 = offs[i], o1 = offs[i + 1];
+    if (o1 - o0 != o0 - p0) return false;
+    for (uint64_t j = 0; j < o1 - o0; ++j)
+      if (keys[o0 + j] != keys[p0 + j]) return false;
+    return true;
   }
 };
 

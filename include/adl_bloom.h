@@ -96,6 +96,19 @@ int adl_bloom_build_segmented_device(const uint8_t *d_keys, const uint64_t *d_of
                                      uint8_t *d_bitmaps, const uint64_t *bitmap_off,
                                      void *d_workspace, uint64_t workspace_bytes, void *stream);
 
+/* Flags for adl_bloom_build_segmented_device_ex. */
+#define ADL_BLOOM_SKIP_ADJACENT_DUPLICATES 1u /* a key equal to the previous key of its
+  filter is not hashed: same bitmap (OR is idempotent, and m still counts every key
+  as Keys2Block's keys.size() does), less work when versions of one user key arrive
+  in a row (memtable order, src/keys.cpp:61-74; SSTableWriter::Add, src/sstable.cpp:28) */
+
+/* adl_bloom_build_segmented_device with flags (0 = identical to it). */
+int adl_bloom_build_segmented_device_ex(const uint8_t *d_keys, const uint64_t *d_offsets,
+                                        uint32_t key_stride, const uint64_t *key_begin,
+                                        uint32_t num_filters, int32_t bits_per_key,
+                                        uint8_t *d_bitmaps, const uint64_t *bitmap_off, uint32_t flags,
+                                        void *d_workspace, uint64_t workspace_bytes, void *stream);
+
 /* Host-pointer convenience: upload keys, build, download exactly
  * adl_bloom_bitmap_bytes(n, bpk) bytes into h_bitmap (which may be unaligned,
  * e.g. the tail of a std::string as in Keys2Block).  Synchronous. */

@@ -599,3 +599,32 @@ def test_filter_cache_lru_and_errors(dev, ab, oracle):
     assert got.all()
     small.close()
     cache.close()
+
+
+# ------------------------------------------------ adjacent duplicate keys skipped (§8f rank 4)
+@pytest.mark.parametrize("shape", ["k16", "stride24", "varlen"])
+def test_build_skip_adjacent_duplicates(dev, ab, oracle, shape):
+    """Runs of equal keys (versions of one user key, memtable order): with
+    ADL_BLOOM_SKIP_ADJACENT_DUPLICATES the bitmaps equal the reference's over
+    ALL keys (m counts the duplicates too), including runs that straddle a
+    filter boundary (the first key of a filter is never skipped)."""
+    rng = np.random.default_rng({"k16": 1, "stride24": 2, "varlen": 3}[shape])
+    reps = rng.integers(1, 6, size=12000)
+    kb = np.array([0, 1, 7000, 7000, 20000, int(reps.sum())], dtype=np.uint64)
+    if shape == "varlen":
+        base = rand_keys(random.Random(4), len(reps), 0, 40) + [b""]
+        keys = [base[i] for i in range(len(reps)) for _ in range(reps[i])]
+        keys[5:8] = [b"", b"", b""]  # equal empty keys
+        dk, do, data, offs = packed_dev(dev, keys)
+        out, boff, sizes = ab.build_segmented(dk, kb, offsets=do, flags=ab.SKIP_ADJACENT_DUPLICATES)
+        want = [oracle.keys2block(data, offsets=offs[int(kb[f]):int(kb[f + 1]) + 1]) for f in range(len(kb) - 1)]
+    else:
+        w = 16 if shape == "k16" else 24
+        base = rng.integers(0, 256, size=(len(reps), w), dtype=np.uint8)
+        keys = np.repeat(base, reps, axis=0)
+        out, boff, sizes = ab.build_segmented(to_dev(dev, keys), kb, flags=ab.SKIP_ADJACENT_DUPLICATES)
+        want = [oracle.keys2block(keys[int(kb[f]):int(kb[f + 1])]) for f in range(len(kb) - 1)]
+    out = out.cpu().numpy()
+    for f in range(len(kb) - 1):
+        got = out[int(boff[f]):int(boff[f]) + int(sizes[f])]
+        assert np.array_equal(got, want[f]), f
