@@ -628,3 +628,17 @@ def test_build_skip_adjacent_duplicates(dev, ab, oracle, shape):
     for f in range(len(kb) - 1):
         got = out[int(boff[f]):int(boff[f]) + int(sizes[f])]
         assert np.array_equal(got, want[f]), f
+
+
+def test_build_maximum_filter(dev, ab, oracle):
+    """The largest filter the reference's int arithmetic allows at bpk 10:
+    n = 26,843,544 keys, m = (n*10+7)*8 = 2,147,483,576 bits (2,048 tiles),
+    bit-identical to the oracle; one key more is ADL_ERR_TOO_LARGE."""
+    n = 26_843_544
+    assert ab.bitmap_bytes(n, 10) * 8 <= 2**31 - 1 and ab.bitmap_bytes(n + 1, 10) == 0
+    keys = ab.synth_keys16(n, seed=0xB16)
+    got = ab.build(keys).cpu().numpy()
+    want = oracle.keys2block(keys.cpu().numpy())
+    assert got.size == want.size == n * 10 + 7
+    assert hashlib.sha256(got.tobytes()).hexdigest() == hashlib.sha256(want.tobytes()).hexdigest()
+    del keys
