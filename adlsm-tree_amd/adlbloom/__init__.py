@@ -44,6 +44,7 @@ EXPORTS = (
     "adl_bloom_murmur3_device", "adl_bloom_murmur3", "adl_synth_keys16_device",
     "adl_synth_varlen_lengths_device", "adl_synth_varlen_fill_device",
     "adl_bloom_profile_enable", "adl_bloom_profile_collect", "adl_synth_probe_queries_device",
+    "adl_bloom_profile_each",
 )
 
 _LIB = None
@@ -105,6 +106,7 @@ def lib() -> ctypes.CDLL:
         "adl_synth_probe_queries_device": (ctypes.c_int, [vp, vp, vp, u64, u64, u64, u32, u64, u64, vp]),
         "adl_bloom_profile_enable": (ctypes.c_int, [u32]),
         "adl_bloom_profile_collect": (ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(u32)]),
+        "adl_bloom_profile_each": (ctypes.c_int, [ctypes.POINTER(ctypes.c_double), u32, ctypes.POINTER(u32)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -344,6 +346,14 @@ def murmur3(seed: int, data: bytes) -> int:
 def profile_enable(capacity: int = 4096) -> None:
     """Start per-kernel HIP-event timing of builds issued by this thread."""
     _check(lib().adl_bloom_profile_enable(capacity), "adl_bloom_profile_enable")
+
+
+def profile_each(capacity: int = 4096):
+    """-> [(pass A ms, pass B ms)] per timed launch pair so far (timing keeps running)."""
+    buf = (ctypes.c_double * (2 * capacity))()
+    n = ctypes.c_uint32(0)
+    _check(lib().adl_bloom_profile_each(buf, capacity, ctypes.byref(n)), "adl_bloom_profile_each")
+    return [(buf[2 * i], buf[2 * i + 1]) for i in range(n.value)]
 
 
 def profile_collect():

@@ -1219,6 +1219,22 @@ int adl_bloom_profile_enable(uint32_t capacity) {
   }
 }
 
+int adl_bloom_profile_each(double *ms_ab, uint32_t capacity, uint32_t *launch_pairs) {
+  if (!ms_ab || !launch_pairs) return ADL_ERR_INVALID_ARG;
+  const uint32_t n = std::min(t_prof.used, capacity);
+  for (uint32_t i = 0; i < n; ++i) {
+    hipEvent_t *e = &t_prof.ev[4 * i];
+    float a = 0.f, b = 0.f;
+    ADL_HIP_TRY(hipEventSynchronize(e[3]));
+    ADL_HIP_TRY(hipEventElapsedTime(&a, e[0], e[1]));
+    ADL_HIP_TRY(hipEventElapsedTime(&b, e[2], e[3]));
+    ms_ab[2 * i] = a;
+    ms_ab[2 * i + 1] = b;
+  }
+  *launch_pairs = n;
+  return ADL_OK;
+}
+
 int adl_bloom_profile_collect(double *ms, uint32_t *builds) {
   if (!ms || !builds) return ADL_ERR_INVALID_ARG;
   ms[0] = ms[1] = 0.0;

@@ -26,6 +26,8 @@ import os
 import sys
 import time
 
+import numpy as np
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "adlsm-tree_amd"))
 
@@ -439,6 +441,7 @@ def main():
             ev[i][1].record()
     barrier()
     elapsed = time.perf_counter() - t0
+    pairs = ab.profile_each(max(args.steps, 1) * 64)
     ms_a, ms_b, nb = ab.profile_collect()
     probe_ms = sum(a.elapsed_time(b) for a, b in ev) / max(args.steps, 1) if probe else 0.0
 
@@ -464,6 +467,16 @@ def main():
             kernels = {"bloom_bin_kernel": round(ms_a / max(args.steps, 1) * 1e3, 2),
                        "bloom_tile_kernel": round(ms_b / max(args.steps, 1) * 1e3, 2)}
             kname = "bloom_bin_kernel + bloom_tile_kernel (one build = the pair)"
+            # median over the steps: each step's launch pairs summed
+            per = len(pairs) // max(args.steps, 1)
+            if per and len(pairs) == per * args.steps:
+                steps_ms = [[sum(p[j] for p in pairs[i * per:(i + 1) * per]) for j in (0, 1)]
+                            for i in range(args.steps)]
+                med = {"bloom_bin_kernel": round(float(np.median([x[0] for x in steps_ms])) * 1e3, 2),
+                       "bloom_tile_kernel": round(float(np.median([x[1] for x in steps_ms])) * 1e3, 2),
+                       "build": round(float(np.median([x[0] + x[1] for x in steps_ms])) * 1e3, 2)}
+            else:
+                med = None
         timed = kern_ms > 0 and (probe or nb)
         achieved = w.bytes_per_launch / (kern_ms * 1e-3) / 1e9 if timed else None
         traffic = load_traffic(args.workload, w.bytes_per_launch)
@@ -498,6 +511,8 @@ def main():
                 "kernel": kname,
                 "algorithmic_bytes_per_step": w.bytes_per_launch,
                 "us_per_step": kernels,
+                "median_us_per_step": None if probe else med,
+                "zero_fill_us": None if probe else 0.0,  # none: pass B writes every bitmap byte
                 "launch_pairs_per_build": None if probe else round(nb / max(args.steps, 1), 2),
                 "read_only_frac": round(16 * w.n / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
                 if (timed and args.workload in ("single", "compaction")) else None,

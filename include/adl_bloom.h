@@ -286,6 +286,10 @@ int adl_bloom_murmur3(uint32_t seed, const void *data, uint64_t len, uint32_t *h
  * to *builds, and disables timing.  Used by bench.py for the live roofline. */
 int adl_bloom_profile_enable(uint32_t capacity);
 int adl_bloom_profile_collect(double *ms, uint32_t *builds);
+/* The same timings one launch pair at a time, without stopping: ms_ab[2i] =
+ * pass A and ms_ab[2i+1] = pass B of pair i, for up to `capacity` pairs (for
+ * medians); call before adl_bloom_profile_collect. */
+int adl_bloom_profile_each(double *ms_ab, uint32_t capacity, uint32_t *launch_pairs);
 
 /* ---------------------------------------------------------------- synthetic data */
 
