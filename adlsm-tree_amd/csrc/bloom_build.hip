@@ -203,6 +203,7 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin_kernel(BuildArgs a, Keys keys
   KeyRegs<Keys> cur[KPT];
   if (slot < total_chunks) fetch(slot, cur);
   for (uint32_t i = tid; i < a.hist_words; i += BLOCK) hist[i] = 0;
+  STAMP_DECL
 
   for (uint32_t r = 0; r < rounds; ++r) {
     const uint32_t wg = r * G + slot;
@@ -246,6 +247,7 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin_kernel(BuildArgs a, Keys keys
       __syncthreads();
 #pragma unroll
       for (int i = 0; i < KPT; ++i) kidx[i] = slot_pos(i) < cnt ? perm[slot_pos(i)] : 0u;
+      STAMP(0);
     } else {
 #pragma unroll
       for (int i = 0; i < KPT; ++i) kidx[i] = tid + i * BLOCK;
@@ -277,6 +279,7 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin_kernel(BuildArgs a, Keys keys
             pending |= 1u << i;
           }
         }
+        STAMP(1);  // setup: key starts and lengths
         uint64_t wb = A0;
         // each window starts at a pending key, so it makes progress; the
         // bound is belt and braces (left-over keys are hashed from global)
@@ -290,6 +293,7 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin_kernel(BuildArgs a, Keys keys
             reinterpret_cast<uint8_t *>(lpos)[nv * 16 + tid] = keys.keys[wb + nv * 16 + tid];
           if (tid == 0) wmin[0] = 0xffffffffu;
           __syncthreads();  // window staged
+          STAMP(6);
           const uint32_t wlo = (uint32_t)(wb - A0), whi = (uint32_t)(we - A0);
 #pragma unroll
           for (int i = 0; i < KPT; ++i) {
@@ -308,6 +312,7 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin_kernel(BuildArgs a, Keys keys
           __syncthreads();  // window consumed; wmin = earliest pending key
           const uint32_t nxt = wmin[0];
           __syncthreads();  // everyone has read wmin before it is reset
+          STAMP(7);
           if (nxt == 0xffffffffu) break;
           wb = A0 + (nxt & ~15u);
         }
@@ -343,6 +348,7 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin_kernel(BuildArgs a, Keys keys
       }
     }
     __syncthreads();  // hist cleared (previous iteration / prologue); staging area free
+    STAMP(1);
 
     constexpr int KR = KFIX > 0 ? KFIX : 1;
     uint32_t pos[KPT][KR];
@@ -364,6 +370,7 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin_kernel(BuildArgs a, Keys keys
       }
     }
     __syncthreads();
+    STAMP(2);
 
     // Exclusive scan: hist[t] = start of tile t's run; hist[T] = k * live keys.
     const uint32_t total = block_excl_scan_array<BLOCK>(hist, T + 1, scratch);
@@ -372,6 +379,7 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin_kernel(BuildArgs a, Keys keys
     uint32_t *tab = table_ws + d.table_base;
     for (uint32_t t = tid; t <= T; t += BLOCK) tab[(uint64_t)t * d.chunks + w] = hist[t];
     __syncthreads();
+    STAMP(3);
 
     // Scatter tile offsets into LDS by tile (hist now serves as the cursor).
 #pragma unroll
@@ -394,6 +402,7 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin_kernel(BuildArgs a, Keys keys
       }
     }
     __syncthreads();
+    STAMP(4);
 
     // Stream the sorted chunk out to region w (a.cap positions, 16-byte
     // aligned).  The hist is cleared for the next chunk meanwhile.
@@ -404,12 +413,14 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin_kernel(BuildArgs a, Keys keys
     uint4 *dst4 = reinterpret_cast<uint4 *>(dst);
     for (uint32_t i = tid; i < nvec; i += BLOCK) dst4[i] = src4[i];
     for (uint32_t i = (nvec << 2) + tid; i < total; i += BLOCK) dst[i] = lpos[i];
+    STAMP(5);
 
     if constexpr (PF) {
 #pragma unroll
       for (int i = 0; i < KPT; ++i) cur[i] = nxt[i];
     }
   }
+  STAMP_FLUSH(0);
 }
 
 // Pass A for the hot path (16-byte keys, compile-time k).  Same output as

@@ -39,7 +39,12 @@ __device__ __forceinline__ uint32_t mix_block(uint32_t h, uint32_t k) {
   k = rotl_quirk<15>(k);  // :32
   k *= 0x1b873593u;       // :33
   h ^= k;                 // :35
-  return rotl_quirk<13>(h) * 5u + 0xe6546b64u;  // :36
+  // :36, h*5 + c as shift + 3-input add: an opaque shift keeps the compiler
+  // from fusing it back into a 64-bit v_mad_u64_u32
+  const uint32_t r = rotl_quirk<13>(h);
+  uint32_t r4 = r << 2;
+  asm("" : "+v"(r4));
+  return r4 + r + 0xe6546b64u;
 }
 
 __device__ __forceinline__ uint32_t mix_tail(uint32_t h, uint32_t k1) {

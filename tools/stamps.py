@@ -23,13 +23,23 @@ NAMES = {
     0: ["loop-top (clear, hash)", "count+store(prev)", "scan", "table", "scatter", "epilogue", "-", "-"],
     1: ["tile start", "stage segs", "gather+or", "write+zero tile", "-", "-", "-", "-"],
 }
+# the generic pass A (bloom_bin_kernel: variable-length keys, WORKLOAD=varlen)
+NAMES_GENERIC = ["length sort", "hash setup / rest", "count", "scan+table", "scatter", "store", "window load",
+                 "window hash"]
 
 
 def main():
     n = int(os.environ.get("N", 10_000_000))
-    keys = adlbloom.synth_keys16(n, seed=0x5EED, device="cuda:0")
-    for _ in range(3):
-        bm = adlbloom.build(keys, bits_per_key=10)
+    varlen = os.environ.get("WORKLOAD", "single") == "varlen"
+    if varlen:
+        NAMES[0] = NAMES_GENERIC
+        data, offs = adlbloom.synth_varlen(n)
+        for _ in range(3):
+            bm = adlbloom.build(data, offsets=offs, bits_per_key=10)
+    else:
+        keys = adlbloom.synth_keys16(n, seed=0x5EED, device="cuda:0")
+        for _ in range(3):
+            bm = adlbloom.build(keys, bits_per_key=10)
     torch.cuda.synchronize()
     L = adlbloom.lib()
     L.adl_bloom_debug_stamps.restype = ctypes.c_int
