@@ -23,9 +23,12 @@ constexpr uint32_t kSeed2 = 0xbaea8a8fu;  // src/filter_block.cpp:23
 // whose sign bit is set sign-extends over every byte above it.
 __device__ __forceinline__ uint32_t quirk_word(uint32_t raw) {
   uint32_t s = raw & 0x80808080u;
-  uint32_t lowest = s & (0u - s);            // sign bit of the lowest negative byte
-  uint32_t fill = ~((lowest << 1) - 1u);     // all bits above that byte (0 if none)
-  return raw | fill;
+  uint32_t lowest = s & (0u - s);  // sign bit of the lowest negative byte
+  // all bits above that byte (0 if none): ~((lowest << 1) - 1) == (0 - lowest) << 1,
+  // kept in that form (one v_lshl_or_b32 with raw) by an opaque negation
+  uint32_t neg = 0u - lowest;
+  asm("" : "+v"(neg));
+  return raw | (neg << 1);
 }
 
 // rotate_left(int value, 15|13) with arithmetic >> (src/murmur3_hash.cpp:5-9).
