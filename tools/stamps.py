@@ -55,6 +55,15 @@ def main():
                 continue
             col = rows[:, i].astype(np.float64)
             print(f"  {NAMES[p][i]:22s} mean {col.mean():9.0f}  max {col.max():9.0f}  ({100 * col.mean() / tot:5.1f} %)")
+    if os.environ.get("DETAIL"):
+        for p in (0, 1):
+            rows = buf[p][:256]
+            tot = rows.sum(axis=1).astype(np.float64)
+            xcd = [tot[x::8].mean() for x in range(8)]
+            print(f"pass {'AB'[p]} per-XCD mean total (blockIdx % 8):", " ".join(f"{v:.0f}" for v in xcd))
+            order = np.argsort(tot)[::-1][:8]
+            print(f"pass {'AB'[p]} slowest workgroups:", " ".join(f"{b}:{tot[b]:.0f}" for b in order))
+            print(f"pass {'AB'[p]} fastest workgroups:", " ".join(f"{b}:{tot[b]:.0f}" for b in np.argsort(tot)[:8]))
     del bm
 
 
