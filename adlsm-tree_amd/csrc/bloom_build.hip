@@ -224,6 +224,31 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin_kernel(BuildArgs a, Keys keys
       return SORT ? (uint32_t)((i * NW + wave) * kWave + lane) : (uint32_t)(tid + i * BLOCK);
     };
     uint32_t kidx[KPT];
+    // Variable-length keys are staged through LDS in windows of wcap bytes at
+    // a fixed stride S = wcap - M (keys of at most M bytes starting in window
+    // w lie wholly inside it; longer keys, and keys past kNWin windows, are
+    // hashed from global memory).  The counting sort orders the chunk's keys
+    // by (window, length class), so the 64 keys of a wave slot share a window
+    // and nearly share a length: each window pass hashes only its own slots,
+    // with lanes of one slot running equally long loops.
+    constexpr uint32_t kNWin = 4;
+    uint64_t A0 = 0, B1 = 0;
+    uint32_t wcap = 0, S = 0, M = 0;
+    bool staged = false;
+    if constexpr (SORT) {
+      const uint64_t kb = d.key_begin + first;
+      A0 = keys.offs[kb] & ~15ull;
+      B1 = keys.offs[kb + cnt];
+      wcap = (4u * k * C - 16u) & ~15u;
+      M = min(4096u, wcap / 2);
+      S = wcap - M;
+      staged = a.stage_keys && wcap >= 64 && B1 - A0 < (1ull << 31);
+    }
+    auto sort_bin = [&](uint64_t o0, uint32_t len) -> uint32_t {
+      if (!staged) return min(len >> 2, 255u);
+      const uint32_t w = (uint32_t)(o0 - A0) / S;
+      return (len > M || w >= kNWin) ? 255u : w * 64u + min(len >> 2, 62u);
+    };
     if constexpr (SORT) {
       for (uint32_t i = tid; i < 256; i += BLOCK) lbin[i] = 0;
       __syncthreads();
@@ -233,7 +258,8 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin_kernel(BuildArgs a, Keys keys
         const uint32_t idx = tid + i * BLOCK;
         if (idx < cnt) {
           const uint64_t ki = d.key_begin + first + idx;
-          lb[i] = min((uint32_t)(keys.offs[ki + 1] - keys.offs[ki]) >> 2, 255u);
+          const uint64_t o0 = keys.offs[ki];
+          lb[i] = sort_bin(o0, (uint32_t)(keys.offs[ki + 1] - o0));
           lr[i] = atomicAdd(&lbin[lb[i]], 1u);
         }
       }
@@ -256,34 +282,27 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin_kernel(BuildArgs a, Keys keys
     uint32_t h1[KPT], h2[KPT];
     if constexpr (SORT) {
       const uint64_t kb = d.key_begin + first;
-      const uint64_t A0 = keys.offs[kb] & ~15ull, B1 = keys.offs[kb + cnt];
-      if (a.stage_keys && B1 - A0 < (1ull << 31)) {
-        // LDS staging: the chunk's packed key bytes pass through the (still
-        // idle) position area in windows of `wcap` bytes, loaded with
-        // coalesced 16-byte loads; every key lying wholly inside the window is
-        // hashed from LDS.  The next window starts at the earliest key not yet
-        // hashed (a key straddling the window's end); a key longer than a
-        // window is hashed straight from global memory.
-        const uint32_t wcap = (4u * k * C - 16u) & ~15u;
+      if (staged) {
         uint4 *stage4 = reinterpret_cast<uint4 *>(lpos);
-        uint32_t *wmin = lbin;  // reused: window bookkeeping (the length sort is done)
-        uint32_t ks0[KPT], klen[KPT];  // key byte start (relative to A0) and length
-        uint32_t pending = 0;           // bit i: slot i still to hash
+        uint32_t ks0[KPT], klen[KPT], kwin[KPT];  // key start (relative to A0), length, window
+        uint32_t pending = 0;                     // bit i: slot i still to hash
 #pragma unroll
         for (int i = 0; i < KPT; ++i) {
           h1[i] = h2[i] = 0;
+          kwin[i] = kNWin;
           if (slot_pos(i) < cnt) {
             const uint64_t o0 = keys.offs[kb + kidx[i]];
             ks0[i] = (uint32_t)(o0 - A0);
             klen[i] = (uint32_t)(keys.offs[kb + kidx[i] + 1] - o0);
+            const uint32_t w = ks0[i] / S;
+            if (klen[i] <= M && w < kNWin) kwin[i] = w;
             pending |= 1u << i;
           }
         }
         STAMP(1);  // setup: key starts and lengths
-        uint64_t wb = A0;
-        // each window starts at a pending key, so it makes progress; the
-        // bound is belt and braces (left-over keys are hashed from global)
-        for (uint32_t iter = 0; wb < B1 && iter <= cnt; ++iter) {
+        const uint32_t nwin = min(kNWin, (uint32_t)((B1 - A0 + S - 1) / S));
+        for (uint32_t win = 0; win < nwin; ++win) {
+          const uint64_t wb = A0 + (uint64_t)win * S;
           const uint64_t we = min(wb + wcap, B1);
           const uint32_t nv = (uint32_t)((we - wb) >> 4);
           const uint4 *src = reinterpret_cast<const uint4 *>(keys.keys + wb);
@@ -291,30 +310,17 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin_kernel(BuildArgs a, Keys keys
           const uint32_t rem = (uint32_t)(we - wb) & 15u;  // last partial vector, bytewise
           if (rem && (uint32_t)tid < rem)
             reinterpret_cast<uint8_t *>(lpos)[nv * 16 + tid] = keys.keys[wb + nv * 16 + tid];
-          if (tid == 0) wmin[0] = 0xffffffffu;
           __syncthreads();  // window staged
           STAMP(6);
-          const uint32_t wlo = (uint32_t)(wb - A0), whi = (uint32_t)(we - A0);
 #pragma unroll
           for (int i = 0; i < KPT; ++i) {
-            if (pending & (1u << i)) {
-              if (ks0[i] >= wlo && ks0[i] + klen[i] <= whi) {
-                hash_lds(lpos, ks0[i] - wlo, klen[i], h1[i], h2[i]);
-                pending &= ~(1u << i);
-              } else if (klen[i] > wcap - 16) {  // longer than any window
-                keys.hash(kb + kidx[i], h1[i], h2[i]);
-                pending &= ~(1u << i);
-              } else {
-                atomicMin(wmin, ks0[i]);
-              }
+            if (kwin[i] == win) {
+              hash_lds(lpos, ks0[i] - win * S, klen[i], h1[i], h2[i]);
+              pending &= ~(1u << i);
             }
           }
-          __syncthreads();  // window consumed; wmin = earliest pending key
-          const uint32_t nxt = wmin[0];
-          __syncthreads();  // everyone has read wmin before it is reset
+          __syncthreads();  // window consumed before the next one overwrites it
           STAMP(7);
-          if (nxt == 0xffffffffu) break;
-          wb = A0 + (nxt & ~15u);
         }
 #pragma unroll
         for (int i = 0; i < KPT; ++i)
