@@ -284,18 +284,19 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin_kernel(BuildArgs a, Keys keys
       const uint64_t kb = d.key_begin + first;
       if (staged) {
         uint4 *stage4 = reinterpret_cast<uint4 *>(lpos);
-        uint32_t ks0[KPT], klen[KPT], kwin[KPT];  // key start (relative to A0), length, window
-        uint32_t pending = 0;                     // bit i: slot i still to hash
+        uint32_t ks0[KPT], klen[KPT];  // key start (relative to A0; ~0 if the slot is
+                                       // empty or hashed from global) and length
+        uint32_t pending = 0;          // bit i: slot i still to hash
 #pragma unroll
         for (int i = 0; i < KPT; ++i) {
           h1[i] = h2[i] = 0;
-          kwin[i] = kNWin;
+          ks0[i] = ~0u;
+          klen[i] = 0;
           if (slot_pos(i) < cnt) {
             const uint64_t o0 = keys.offs[kb + kidx[i]];
-            ks0[i] = (uint32_t)(o0 - A0);
+            const uint32_t rel = (uint32_t)(o0 - A0);
             klen[i] = (uint32_t)(keys.offs[kb + kidx[i] + 1] - o0);
-            const uint32_t w = ks0[i] / S;
-            if (klen[i] <= M && w < kNWin) kwin[i] = w;
+            if (klen[i] <= M && rel < kNWin * S) ks0[i] = rel;
             pending |= 1u << i;
           }
         }
@@ -312,10 +313,11 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin_kernel(BuildArgs a, Keys keys
             reinterpret_cast<uint8_t *>(lpos)[nv * 16 + tid] = keys.keys[wb + nv * 16 + tid];
           __syncthreads();  // window staged
           STAMP(6);
+          const uint32_t wlo = win * S;
 #pragma unroll
           for (int i = 0; i < KPT; ++i) {
-            if (kwin[i] == win) {
-              hash_lds(lpos, ks0[i] - win * S, klen[i], h1[i], h2[i]);
+            if (ks0[i] - wlo < S) {  // starts in this window (unsigned wrap for earlier keys)
+              hash_lds(lpos, ks0[i] - wlo, klen[i], h1[i], h2[i]);
               pending &= ~(1u << i);
             }
           }
