@@ -234,6 +234,7 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin_kernel(BuildArgs a, Keys keys
     constexpr uint32_t kNWin = 4;
     uint64_t A0 = 0, B1 = 0;
     uint32_t wcap = 0, S = 0, M = 0;
+    FastMod divS{};
     bool staged = false;
     if constexpr (SORT) {
       const uint64_t kb = d.key_begin + first;
@@ -243,10 +244,11 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin_kernel(BuildArgs a, Keys keys
       M = min(4096u, wcap / 2);
       S = wcap - M;
       staged = a.stage_keys && wcap >= 64 && B1 - A0 < (1ull << 31);
+      if (staged) divS = fastmod_for(S);
     }
     auto sort_bin = [&](uint64_t o0, uint32_t len) -> uint32_t {
       if (!staged) return min(len >> 2, 255u);
-      const uint32_t w = (uint32_t)(o0 - A0) / S;
+      const uint32_t w = fastdiv((uint32_t)(o0 - A0), divS);
       return (len > M || w >= kNWin) ? 255u : w * 64u + min(len >> 2, 62u);
     };
     if constexpr (SORT) {

@@ -181,6 +181,12 @@ __device__ __forceinline__ FastMod fastmod_for(uint32_t m) {
   return f;
 }
 
+// h / m with the same magic numbers.
+__device__ __forceinline__ uint32_t fastdiv(uint32_t h, const FastMod &d) {
+  const uint32_t t = __umulhi(h, d.magic);
+  return (t + ((h - t) >> 1)) >> d.shift;
+}
+
 __device__ __forceinline__ uint32_t fastmod(uint32_t h, const FastMod &d) {
   const uint32_t t = __umulhi(h, d.magic);
   const uint32_t q = (t + ((h - t) >> 1)) >> d.shift;
