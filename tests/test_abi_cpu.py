@@ -89,3 +89,38 @@ def test_missing_library_fails_loudly(monkeypatch, tmp_path):
     monkeypatch.setattr(adlbloom, "LIB_PATH", str(tmp_path / "nope.so"))
     with pytest.raises(RuntimeError):
         adlbloom.lib()
+
+
+def test_filter_block_bytes_matches_oracle_framing(oracle):
+    """adl_bloom_filter_block_bytes (host arithmetic only) equals the length of
+    the block FilterBlockWriter::Final writes (oracle framing, src/filter_block.cpp:77-102)."""
+    import numpy as np
+
+    import adlbloom
+
+    rng = np.random.default_rng(3)
+    for nf in (0, 1, 2, 7, 65, 200):
+        for bpk in (1, 10, 23):
+            sizes = rng.integers(0, 3000, size=nf)
+            kb = np.concatenate([[0], np.cumsum(sizes)]).astype(np.uint64)
+            want = len(oracle.filter_block_final([bytes(oracle.bitmap_bytes(int(n), bpk)) for n in sizes], bpk))
+            assert adlbloom.filter_block_bytes(kb, bpk) == want
+    # beyond the reference's int offsets -> 0
+    kb = (np.arange(10, dtype=np.uint64) * 26_000_000)  # 9 valid filters, 2.34 GB together
+    assert adlbloom.filter_block_bytes(kb[:8], 10) > 0
+    assert adlbloom.filter_block_bytes(kb, 10) == 0
+
+
+def test_segmented_ex_rejects_unknown_flags():
+    """Argument checks run before any device call (no GPU here)."""
+    import ctypes
+
+    import adlbloom
+
+    L = adlbloom.lib()
+    kb = (ctypes.c_uint64 * 2)(0, 16)
+    off = (ctypes.c_uint64 * 1)(0)
+    buf = ctypes.create_string_buffer(64)
+    rc = L.adl_bloom_build_segmented_device_ex(ctypes.addressof(buf), None, 16, kb, 1, 10,
+                                               ctypes.addressof(buf), off, 0x80, None, 0, None)
+    assert rc == -1  # ADL_ERR_INVALID_ARG
