@@ -33,12 +33,22 @@ __global__ __launch_bounds__(kBlock) void gather(const uint32_t *__restrict__ po
 #pragma unroll
         for (int u = 0; u < kInFlight; ++u) {
           const uint32_t c = c0 + u * kWaves;
-          const uint32_t *sp = pos + (uint64_t)c * cap + (uint64_t)t * len;
-          v[u] = (c < W && (uint32_t)lane < len) ? sp[lane] : 0u;
+          const uint32_t cc = c < W ? c : W - 1;
+          const uint32_t *sp = pos + (uint64_t)cc * cap + (uint64_t)t * len;
+          if (X4 == 3) {
+            v[u] = sp[lane];  // every lane loads (the real pass B's first stage)
+          } else if (X4 == 4) {
+            // bounds-checked buffer load: lanes past len return 0 with no memory access
+            const __amdgpu_buffer_rsrc_t r =
+                __builtin_amdgcn_make_buffer_rsrc((void *)sp, 0, c < W ? len * 4 : 0, 0x00020000);
+            v[u] = __builtin_amdgcn_raw_buffer_load_b32(r, lane * 4, 0, 0);
+          } else {
+            v[u] = (c < W && (uint32_t)lane < len) ? sp[lane] : 0u;
+          }
         }
 #pragma unroll
         for (int u = 0; u < kInFlight; ++u) {
-          if (X4 == 2) {
+          if (X4 >= 2) {
             if (c0 + u * kWaves < W && (uint32_t)lane < len) atomicOr(&tile[(v[u] >> 5) & 32767], 1u << (v[u] & 31));
           } else {
             acc += v[u];
@@ -62,7 +72,7 @@ __global__ __launch_bounds__(kBlock) void gather(const uint32_t *__restrict__ po
       }
     }
   }
-  if (X4 == 2) {
+  if (X4 >= 2) {
     __syncthreads();
     acc = tile[threadIdx.x * 31];
   }
@@ -89,22 +99,26 @@ int main() {
     free(h);
   }
   CK(hipFuncSetAttribute((const void *)gather<2>, hipFuncAttributeMaxDynamicSharedMemorySize, 131072));
+  CK(hipFuncSetAttribute((const void *)gather<3>, hipFuncAttributeMaxDynamicSharedMemorySize, 131072));
+  CK(hipFuncSetAttribute((const void *)gather<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 131072));
   CK(hipMalloc(&sink, 1 << 16));
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
-  printf("%5s %6s %12s %12s %12s  (useful GB/s; %u regions x %u tiles)\n", "len", "remap", "dword", "dwordx4",
-         "dword+ds_or", W, tiles);
-  for (uint32_t remap : {0u, 1u})
-  for (uint32_t len : {32u, 44u, 64u}) {
-    float gbs[3];
-    for (int v = 0; v < 3; ++v) {
+  printf("%5s %6s %12s %12s %12s %12s %12s  (useful GB/s; %u regions x %u tiles)\n", "len", "remap", "dword",
+         "dwordx4", "dword+ds_or", "all64+ds_or", "buf+ds_or", W, tiles);
+  for (uint32_t remap : {1u})
+  for (uint32_t len : {32u, 44u, 53u, 64u}) {
+    float gbs[5];
+    for (int v = 0; v < 5; ++v) {
       float best = 1e30f;
       for (int rep = 0; rep < 5; ++rep) {
         CK(hipEventRecord(e0, 0));
         if (v == 0) hipLaunchKernelGGL(gather<0>, dim3(cus), dim3(kBlock), 0, 0, pos, W, cap, len, tiles, remap, sink);
         else if (v == 1) hipLaunchKernelGGL(gather<1>, dim3(cus), dim3(kBlock), 0, 0, pos, W, cap, len, tiles, remap, sink);
-        else hipLaunchKernelGGL(gather<2>, dim3(cus), dim3(kBlock), 131072, 0, pos, W, cap, len, tiles, remap, sink);
+        else if (v == 2) hipLaunchKernelGGL(gather<2>, dim3(cus), dim3(kBlock), 131072, 0, pos, W, cap, len, tiles, remap, sink);
+        else if (v == 3) hipLaunchKernelGGL(gather<3>, dim3(cus), dim3(kBlock), 131072, 0, pos, W, cap, len, tiles, remap, sink);
+        else hipLaunchKernelGGL(gather<4>, dim3(cus), dim3(kBlock), 131072, 0, pos, W, cap, len, tiles, remap, sink);
         CK(hipEventRecord(e1, 0));
         CK(hipEventSynchronize(e1));
         float ms;
@@ -113,7 +127,7 @@ int main() {
       }
       gbs[v] = (float)((double)W * tiles * len * 4 / (best * 1e-3) / 1e9);
     }
-    printf("%5u %6u %12.0f %12.0f %12.0f\n", len, remap, gbs[0], gbs[1], gbs[2]);
+    printf("%5u %6u %12.0f %12.0f %12.0f %12.0f %12.0f\n", len, remap, gbs[0], gbs[1], gbs[2], gbs[3], gbs[4]);
   }
   return 0;
 }
