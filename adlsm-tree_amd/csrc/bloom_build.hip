@@ -80,7 +80,8 @@ struct BuildArgs {
   uint32_t dyn_tiles;  // pass B: tiles from a work queue that pass A resets (ADL_BLOOM_DYN_TILES)
   uint32_t stage_keys; // pass A: LDS-staged variable-length keys (16-B aligned key buffer; ADL_BLOOM_STAGE_KEYS)
   uint32_t dedup;      // skip a key equal to its predecessor in the same filter (ADL_BLOOM_SKIP_ADJACENT_DUPLICATES)
-  uint32_t exp;        // diagnostics build only (ADL_BLOOM_EXP bits, wrong results): 1 no hash, 2 no stores
+  uint32_t exp;        // diagnostics build only (ADL_BLOOM_EXP bits, wrong results): pass A 1 no hash,
+                       // 2 no position stores; pass B 4 no ds_or, 8 no bitmap stores
   FilterDesc f[kMaxFilters];
 };
 
@@ -628,7 +629,16 @@ __global__ __launch_bounds__(kBlockB) void bloom_tile_kernel(BuildArgs a,
       }
     }
   };
+#ifdef ADL_BLOOM_STAMPS
+  // diagnostics (ADL_BLOOM_EXP, wrong bitmaps): 4 = no ds_or (plain sum), 8 = no bitmap stores
+  uint32_t exp_sink = 0;
+  auto or_pos = [&](uint32_t off) {
+    if (a.exp & 4) exp_sink += off;
+    else atomicOr(&tile[off >> 5], 1u << (off & 31));
+  };
+#else
   auto or_pos = [&](uint32_t off) { atomicOr(&tile[off >> 5], 1u << (off & 31)); };
+#endif
 
   // Round r covers tiles [r*G, (r+1)*G); inside a round each XCD takes G/8
   // consecutive tiles, so the line a tile's segment shares with its
@@ -768,6 +778,9 @@ __global__ __launch_bounds__(kBlockB) void bloom_tile_kernel(BuildArgs a,
       const uint4 v = t4[i];
       t4z[i] = make_uint4(0, 0, 0, 0);
       if (i < nvec) {
+#ifdef ADL_BLOOM_STAMPS
+        if (a.exp & 8) continue;
+#endif
         if (a.nt_bitmap) store_nt(out4 + i, v);
         else out4[i] = v;
       }
@@ -776,6 +789,9 @@ __global__ __launch_bounds__(kBlockB) void bloom_tile_kernel(BuildArgs a,
     STAMP(3);
     wg = next;
   }
+#ifdef ADL_BLOOM_STAMPS
+  if (exp_sink == 0x9e3779b9u) tile_queue[1] = exp_sink;  // keeps the diagnostic sum alive
+#endif
   STAMP_FLUSH(1);
 }
 
