@@ -7,7 +7,8 @@ Sources (never the restatement under test):
   * appendix_b.json: SURVEY.md Appendix B, produced during the survey by the
     compiled reference src/filter_block.cpp + src/murmur3_hash.cpp (bitmap
     SHA-256s / popcounts for SplitMix64 keys, probe false-positive counts and
-    masks, the test/filter_block_test.cpp block).  Transcribed here verbatim.
+    masks, the test/filter_block_test.cpp block, the test/sstable_test.cpp
+    SSTable oid and size).  Transcribed here verbatim.
 
 Run: python tests/golden/make_golden.py
 """
@@ -78,6 +79,12 @@ APPENDIX_B = {
         "bytes": 100111,
         "sha256": "68cb3322ec5d66d7dbd58781011cb955a62f31a89e7a41d3d3aca4e458ace57e",
         "last30_hex": "00010000000000cf860100f48601000200000062663a0a00000007000000",
+    },
+    "sstable_test": {
+        "scenario": "test/sstable_test.cpp:9-27 BuildSSTable (10,000 x key{i}/value{i}, seq=i, OP_PUT), "
+                    "MemTable::BuildSSTable -> SSTableWriter, bits_per_key=10",
+        "oid": "15c52c5634ae0b6eb9529a93c797a4acd1cfbde1a7a85a33565d99c4f5a2d8a6",
+        "bytes": 420270,
     },
     "murmur3_kat": [
         {"key": "", "h1": "389d2042", "h2": "1f2c6e1c"},

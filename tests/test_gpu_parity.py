@@ -642,3 +642,28 @@ def test_build_maximum_filter(dev, ab, oracle):
     assert got.size == want.size == n * 10 + 7
     assert hashlib.sha256(got.tobytes()).hexdigest() == hashlib.sha256(want.tobytes()).hexdigest()
     del keys
+
+
+# ------------------------------------------------ SSTable build path (§8f rank 1)
+@pytest.mark.parametrize("mode", ["add", "batch"])
+@pytest.mark.parametrize("which", [1, 2])
+def test_sstable_writer_file_parity(dev, golden, oracle, tmp_path, mode, which):
+    """test/sstable_test.cpp memtables flushed through the C++ SSTableWriter,
+    filter built on the GPU: the file is byte-identical to the oracle's
+    restatement, and for BuildSSTable (:9-27) its name is the reference's oid."""
+    import sstable_oracle as S
+
+    exe = os.path.join(ROOT, "adlsm-tree_amd", "bin", "sstable_test")
+    args = [exe] + (["batch"] if mode == "batch" else []) + [str(which), str(tmp_path)]
+    r = subprocess.run(args, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    oid, size = r.stdout.split()
+    files = list(tmp_path.glob("*.sst"))
+    assert [f.name for f in files] == [oid + ".sst"]
+    got = files[0].read_bytes()
+    want = S.sstable_bytes(S.sstable_test_entries(which))
+    assert len(got) == int(size) == len(want)
+    assert got == want
+    assert hashlib.sha256(got).hexdigest() == oid
+    if which == 1:
+        assert oid == golden["appendix_b"]["sstable_test"]["oid"]
