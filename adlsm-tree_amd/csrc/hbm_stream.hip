@@ -38,3 +38,49 @@ extern "C" int adl_hbm_stream_read(const void *d_buf, uint64_t bytes, uint32_t *
                      static_cast<const v4u *>(d_buf), bytes / 16, d_sink);
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }
+
+// Random single-byte reads over a working set of W bytes: the access pattern
+// of the bloom probe (k dependent-free byte loads per query into filters far
+// larger than the Infinity Cache).  Gives bench.py the random-read rate this
+// box reaches, the real ceiling of the probe (its 21 B/query are not what
+// bounds it).  R = 4 independent loads in flight per lane per iteration.
+__device__ __forceinline__ uint32_t rr_mix(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x85ebca6bu;
+  x ^= x >> 13;
+  x *= 0xc2b2ae35u;
+  x ^= x >> 16;
+  return x;
+}
+
+__global__ __launch_bounds__(256) void hbm_random_read_kernel(const uint8_t *__restrict__ p, uint64_t W,
+                                                              uint32_t iters, uint32_t *__restrict__ sink) {
+  uint32_t x = rr_mix(blockIdx.x * 256 + threadIdx.x + 1), acc = 0;
+  for (uint32_t it = 0; it < iters; ++it) {
+    uint32_t v[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      x = x * 1664525u + 1013904223u;
+      v[r] = p[((uint64_t)rr_mix(x) * W) >> 32];
+    }
+    acc += v[0] + v[1] + v[2] + v[3];
+  }
+  if (acc == 0x12345u) sink[blockIdx.x] = acc;  // keeps the loads
+}
+
+// Returns the number of byte reads the launch performs (0 on error).
+extern "C" uint64_t adl_hbm_random_read(const void *d_buf, uint64_t bytes, uint32_t iters, uint32_t *d_sink,
+                                        uint32_t sink_words, void *stream) {
+  if (!d_buf || !d_sink || bytes == 0 || bytes > (1ull << 32) || iters == 0) return 0;
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return 0;
+  uint32_t grid = (uint32_t)cus * 8u;
+  if (grid > sink_words) grid = sink_words;
+  if (grid == 0) return 0;
+  hipLaunchKernelGGL(hbm_random_read_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream,
+                     static_cast<const uint8_t *>(d_buf), bytes, iters, d_sink);
+  if (hipGetLastError() != hipSuccess) return 0;
+  return (uint64_t)grid * 256u * iters * 4u;
+}

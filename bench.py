@@ -262,7 +262,22 @@ def probe_check(w, out):
         t = w.tables[li]
         ref = O.keys2block(O.splitmix_keys16(0x5EED + t, PROBE_KEYS_PER_TABLE), bits_per_key=BPK)
         tab_ok &= bool(np.array_equal(bms[int(off[li]):int(off[li + 1])], ref))
+    # bitmap byte reads per query with the reference's early exit (src/filter_block.cpp:54-59),
+    # counted on the sample: the probe's real work unit (k random reads at most)
+    h = O.murmur3_batch(w.keys[:ns].cpu().numpy())
+    fid = w.fid[:ns].cpu().numpy().astype(np.int64)
+    base = np.asarray(off, dtype=np.int64)[fid]
+    m = (np.asarray(off, dtype=np.int64)[fid + 1] - base) * 8
+    alive = np.ones(ns, dtype=bool)
+    reads = np.zeros(ns, dtype=np.int64)
+    for j in range(O.num_probes(BPK)):
+        pos = ((h[:, 0].astype(np.uint64) + np.uint64(j) * h[:, 1].astype(np.uint64)) % np.uint64(1 << 32)
+               ).astype(np.int64) % m
+        bit = (bms[base + (pos >> 3)] >> (pos & 7)) & 1
+        reads += alive
+        alive &= bit.astype(bool)
     return {"hit_rate_inserted": round(hits_ins / max(n_ins, 1), 6), "false_negatives": n_ins - hits_ins,
+            "bitmap_reads_per_query": round(float(reads.mean()), 4),
             "fpr_fresh": round(fp / max(n_fresh, 1), 6), "queries_inserted": n_ins, "queries_fresh": n_fresh,
             "oracle_sample": f"{ns} queries {'bit-identical' if sample_ok else 'MISMATCH'} vs oracle_probe_multi",
             "oracle_bitmaps": "tables %d,%d %s" % (w.tables[0], w.tables[-1],
@@ -297,6 +312,33 @@ def hbm_stream_read_gbs(nbytes=4 << 30, reps=5):
         best = max(best, nbytes / (e0.elapsed_time(e1) * 1e-3) / 1e9)
     del buf
     return round(best, 1)
+
+
+def hbm_random_read_gps(buf, iters=64, reps=3):
+    """Measured random single-byte read rate (G reads/s) over `buf` (the probe's own
+    filter arena, so the same working set), lib/libadlhbm.so's hbm_random_read_kernel."""
+    import ctypes
+
+    import torch
+
+    L = ctypes.CDLL(os.path.join(ROOT, "adlsm-tree_amd", "lib", "libadlhbm.so"))
+    L.adl_hbm_random_read.restype = ctypes.c_uint64
+    L.adl_hbm_random_read.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_void_p,
+                                      ctypes.c_uint32, ctypes.c_void_p]
+    sink = torch.zeros(1 << 16, dtype=torch.int32, device="cuda")
+    st = torch.cuda.current_stream()
+    best = 0.0
+    for _ in range(reps + 1):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        nreads = L.adl_hbm_random_read(buf.data_ptr(), buf.numel(), iters, sink.data_ptr(), sink.numel(),
+                                       ctypes.c_void_p(st.cuda_stream))
+        e1.record(st)
+        e1.synchronize()
+        if not nreads:
+            return None
+        best = max(best, nreads / (e0.elapsed_time(e1) * 1e-3) / 1e9)
+    return round(best, 2)
 
 
 def e2e(n, iters=5):
@@ -521,6 +563,17 @@ def main():
             },
             "parity": parity,
         }
+        if probe and parity and timed:
+            # the probe's real ceiling: random bitmap byte reads (k per query at most)
+            rr = hbm_random_read_gps(w.bitmaps)
+            gps = parity["bitmap_reads_per_query"] * w.n / (kern_ms * 1e-3) / 1e9
+            out_json["roofline"]["random_reads"] = {
+                "reads_per_query": parity["bitmap_reads_per_query"],
+                "achieved_greads_per_s": round(gps, 2),
+                "measured_random_read_greads_per_s": rr,
+                "frac_of_measured_random_read": round(gps / rr, 4) if rr else None,
+                "working_set_bytes": int(w.bitmaps.numel()),
+            }
         if world == 1 and args.workload == "single" and not args.no_e2e:
             out_json["e2e"] = e2e(w.n)
         if world == 1 and args.workload == "compaction" and not args.no_e2e:
