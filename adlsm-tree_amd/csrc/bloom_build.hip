@@ -80,6 +80,7 @@ struct BuildArgs {
   uint32_t dyn_tiles;  // pass B: tiles from a work queue that pass A resets (ADL_BLOOM_DYN_TILES)
   uint32_t stage_keys; // pass A: LDS-staged variable-length keys (16-B aligned key buffer; ADL_BLOOM_STAGE_KEYS)
   uint32_t dedup;      // skip a key equal to its predecessor in the same filter (ADL_BLOOM_SKIP_ADJACENT_DUPLICATES)
+  uint32_t scan1;      // pass A: one-barrier tile-count scan (ADL_BLOOM_SCAN1)
   uint32_t exp;        // diagnostics build only (ADL_BLOOM_EXP bits, wrong results): pass A 1 no hash,
                        // 2 no position stores; pass B 4 no ds_or, 8 no bitmap stores
   FilterDesc f[kMaxFilters];
@@ -384,7 +385,9 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin_kernel(BuildArgs a, Keys keys
     STAMP(2);
 
     // Exclusive scan: hist[t] = start of tile t's run; hist[T] = k * live keys.
-    const uint32_t total = block_excl_scan_array<BLOCK>(hist, T + 1, scratch);
+    // the table rows below are written by the thread that scanned them
+    const uint32_t total = a.scan1 ? block_excl_scan_array_1b<BLOCK>(hist, T + 1, scratch)
+                                   : block_excl_scan_array<BLOCK>(hist, T + 1, scratch);
 
     // (tile, chunk) table, T+1 rows of W entries: row t = start of tile t.
     uint32_t *tab = table_ws + d.table_base;
@@ -539,7 +542,8 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin16_kernel(BuildArgs a, Keys16 
     __syncthreads();  // counts complete; the previous chunk's LDS copy is read out
     STAMP(1);
 
-    block_excl_scan_array<BLOCK>(hist, T + 1, scratch);
+    if (a.scan1) block_excl_scan_array_1b<BLOCK>(hist, T + 1, scratch);
+    else block_excl_scan_array<BLOCK>(hist, T + 1, scratch);
     STAMP(2);
     uint32_t *tab = table_ws + d.table_base;
 #pragma unroll
@@ -909,6 +913,7 @@ int make_plan(const uint64_t *counts, uint32_t nf, int32_t bpk, Plan &p) {
   p.a.nt_bitmap = env_flag("ADL_BLOOM_NT_BITMAP", 1);
   p.a.dyn_tiles = env_flag("ADL_BLOOM_DYN_TILES", 0);
   p.a.stage_keys = env_flag("ADL_BLOOM_STAGE_KEYS", 1);
+  p.a.scan1 = env_flag("ADL_BLOOM_SCAN1", 1);
 #ifdef ADL_BLOOM_STAMPS
   p.a.exp = env_u32("ADL_BLOOM_EXP", 0);  // diagnostics build only
 #else

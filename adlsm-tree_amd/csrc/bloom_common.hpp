@@ -136,6 +136,42 @@ __device__ __forceinline__ uint32_t block_excl_scan_array(uint32_t *a, uint32_t 
   return total;
 }
 
+// The same in-place exclusive scan with one barrier instead of four: every
+// wave scans its threads' run sums, publishes its total, and after the one
+// barrier each wave adds up the totals of the waves before it itself.  When
+// each thread owns at most one entry (N <= BLOCK), entry i is written and
+// later read back by thread i only, so no barrier follows; otherwise one does.
+template <int BLOCK>
+__device__ __forceinline__ uint32_t block_excl_scan_array_1b(uint32_t *a, uint32_t N, uint32_t *scratch) {
+  constexpr int NW = BLOCK / kWave;
+  const int tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid / kWave;
+  const uint32_t per = (N + BLOCK - 1) / BLOCK;
+  const uint32_t beg = tid * per;
+  const uint32_t end = beg + per < N ? beg + per : N;
+  uint32_t v = 0;
+  for (uint32_t i = beg; i < end; ++i) v += a[i];
+  const uint32_t incl = wave_incl_scan(v, lane);
+  if (lane == kWave - 1) scratch[wave] = incl;
+  __syncthreads();
+  // the totals of waves 0..wave-1: lanes < wave hold one each (all within lanes
+  // 0..NW-1), summed over those lanes and broadcast from lane 0
+  const uint32_t wt = lane < NW ? scratch[lane] : 0u;
+  uint32_t t = lane < wave ? wt : 0u, all = wt;
+#pragma unroll
+  for (int off = 1; off < NW; off <<= 1) {
+    t += __shfl_xor(t, off, kWave);
+    all += __shfl_xor(all, off, kWave);
+  }
+  uint32_t run = __builtin_amdgcn_readfirstlane(t) + incl - v;
+  for (uint32_t i = beg; i < end; ++i) {
+    const uint32_t x = a[i];
+    a[i] = run;
+    run += x;
+  }
+  if (per > 1) __syncthreads();
+  return __builtin_amdgcn_readfirstlane(all);
+}
+
 }  // namespace adl_dev
 
 namespace adl_host {
