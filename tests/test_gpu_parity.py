@@ -667,3 +667,12 @@ def test_sstable_writer_file_parity(dev, golden, oracle, tmp_path, mode, which):
     assert hashlib.sha256(got).hexdigest() == oid
     if which == 1:
         assert oid == golden["appendix_b"]["sstable_test"]["oid"]
+
+
+def test_concurrent_probes_and_builds(dev):
+    """SURVEY.md §8b threading: 8 threads probing one FilterBlockReader while 2
+    threads build filter blocks; every result equals the sequential one."""
+    exe = os.path.join(ROOT, "adlsm-tree_amd", "bin", "concurrency_test")
+    r = subprocess.run([exe, "8", "2", "12"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert " 0 mismatches" in r.stdout
