@@ -37,11 +37,10 @@ __global__ __launch_bounds__(1024) void k(uint32_t *out, int iters, uint32_t wor
 }
 
 template <int OP>
-float run(const char *name, int spread) {
+float run(const char *name, int spread, uint32_t words = 32768) {
   uint32_t *out;
   (void)hipMalloc(&out, 1 << 20);
   const int iters = 256, cus = 256;
-  const uint32_t words = 32768;  // 128 KiB
   hipFuncSetAttribute((const void *)k<OP>, hipFuncAttributeMaxDynamicSharedMemorySize, words * 4);
   hipEvent_t a, b;
   hipEventCreate(&a); hipEventCreate(&b);
@@ -56,13 +55,17 @@ float run(const char *name, int spread) {
   ms /= 5;
   const double instr_per_cu = 16.0 * 16 * iters;  // 16 waves x 16 unroll x iters
   const double ns = ms * 1e6 / instr_per_cu;
-  printf("%-16s spread=%d  %.3f ms  %.2f ns/wave-instr/CU  (%.1f cycles @2.4GHz)  %.2f Gops/s chip\n", name, spread, ms,
-         ns, ns * 2.4, 64.0 * instr_per_cu * cus / (ms * 1e-3) / 1e9);
+  printf("%-16s words=%6u spread=%d  %.3f ms  %.2f ns/wave-instr/CU  (%.1f cycles @2.4GHz)  %.2f Gops/s chip\n", name,
+         words, spread, ms, ns, ns * 2.4, 64.0 * instr_per_cu * cus / (ms * 1e-3) / 1e9);
   (void)hipFree(out);
   return ms;
 }
 
 int main() {
+  // random over 1024 words: the pass-A tile histogram (T+1 = 764 counters at 10 M keys)
+  run<1>("ds_add_u32", 1, 1024);
+  run<2>("ds_add_rtn_u32", 1, 1024);
+  run<4>("ds_read_b32", 1, 1024);
   for (int s = 1; s >= 0; --s) {
     run<0>("ds_or_b32", s);
     run<1>("ds_add_u32", s);
