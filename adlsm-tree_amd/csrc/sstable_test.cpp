@@ -5,6 +5,9 @@
 //   sstable_test <which 1|2> <dir>   writes <dir>/<oid>.sst, prints "<oid> <bytes>"
 //   sstable_test batch <which> <dir> the same through AddBatch (packed run)
 //   sstable_test sha256 <file>       the writer's SHA-256 of a file (CPU only)
+//   sstable_test bench <n> <dir>     flush an n-entry memtable ("key%012d" / 100-byte
+//                                    values, seq = i): prints one JSON line with the
+//                                    time of the Add loop and of Final (GPU filter)
 //
 // tests/test_gpu_parity.py compares the file byte for byte with the oracle
 // (oracle/sstable_oracle.py) and the oid with SURVEY.md Appendix B.
@@ -13,6 +16,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <fstream>
 #include <sstream>
 #include <string>
@@ -73,6 +77,47 @@ int main(int argc, char **argv) {
     unsigned char d[32];
     h.Final(d);
     printf("%s\n", Sha256Hex(d).c_str());
+    return 0;
+  }
+  if (argc == 4 && !strcmp(argv[1], "bench")) {
+    const long n = atol(argv[2]);
+    std::vector<Entry> mem;
+    mem.reserve(n);
+    char buf[32];
+    for (long i = 0; i < n; ++i) {
+      snprintf(buf, sizeof buf, "key%012ld", i);
+      mem.push_back({buf, (int64_t)i, 0, std::string(100, (char)('a' + i % 26))});
+    }
+    std::vector<std::string> ikeys;
+    ikeys.reserve(n);
+    for (const auto &e : mem) ikeys.push_back(InnerKey(e));
+    double best_add = 1e30, best_final = 1e30, best_filter = 1e30;
+    int size = 0;
+    std::string oid;
+    for (int rep = 0; rep < 4; ++rep) {  // rep 0 warms the device up
+      StringSink sink;
+      SSTableWriter w(&sink, 10);
+      const auto t0 = std::chrono::steady_clock::now();
+      for (long i = 0; i < n; ++i)
+        if (w.Add(ikeys[i], mem[i].value)) return 1;
+      const auto t1 = std::chrono::steady_clock::now();
+      unsigned char d[32];
+      if (w.Final(d)) return 1;
+      const auto t2 = std::chrono::steady_clock::now();
+      if (rep) {
+        best_add = std::min(best_add, std::chrono::duration<double>(t1 - t0).count());
+        best_final = std::min(best_final, std::chrono::duration<double>(t2 - t1).count());
+        best_filter = std::min(best_filter, w.filter_seconds());
+      }
+      size = w.GetFileSize();
+      oid = Sha256Hex(d);
+      if (rep == 3) {  // keep one file for the caller's parity check
+        std::ofstream(std::string(argv[3]) + "/" + oid + ".sst", std::ios::binary)
+            .write(sink.data().data(), (std::streamsize)sink.data().size());
+      }
+    }
+    printf("{\"entries\": %ld, \"bytes\": %d, \"oid\": \"%s\", \"add_s\": %.6f, \"final_s\": %.6f, \"filter_s\": %.6f}\n",
+           n, size, oid.c_str(), best_add, best_final, best_filter);
     return 0;
   }
   int a = 1;

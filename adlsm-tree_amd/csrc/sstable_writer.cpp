@@ -11,6 +11,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <chrono>
 
 namespace adl {
 
@@ -81,66 +82,20 @@ RC FooterBlockWriter::Final(string &result) {
 }
 
 // ------------------------------------------------------------ SHA-256
-namespace {
-constexpr uint32_t kK[64] = {
-    0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4, 0xab1c5ed5,
-    0xd807aa98, 0x12835b01, 0x243185be, 0x550c7dc3, 0x72be5d74, 0x80deb1fe, 0x9bdc06a7, 0xc19bf174,
-    0xe49b69c1, 0xefbe4786, 0x0fc19dc6, 0x240ca1cc, 0x2de92c6f, 0x4a7484aa, 0x5cb0a9dc, 0x76f988da,
-    0x983e5152, 0xa831c66d, 0xb00327c8, 0xbf597fc7, 0xc6e00bf3, 0xd5a79147, 0x06ca6351, 0x14292967,
-    0x27b70a85, 0x2e1b2138, 0x4d2c6dfc, 0x53380d13, 0x650a7354, 0x766a0abb, 0x81c2c92e, 0x92722c85,
-    0xa2bfe8a1, 0xa81a664b, 0xc24b8b70, 0xc76c51a3, 0xd192e819, 0xd6990624, 0xf40e3585, 0x106aa070,
-    0x19a4c116, 0x1e376c08, 0x2748774c, 0x34b0bcb5, 0x391c0cb3, 0x4ed8aa4a, 0x5b9cca4f, 0x682e6ff3,
-    0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7, 0xc67178f2};
-inline uint32_t ror(uint32_t x, int c) { return (x >> c) | (x << (32 - c)); }
-}  // namespace
-
-Sha256::Sha256()
-    : h_{0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a, 0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19} {}
-
-void Sha256::Block(const unsigned char *p) {
-  uint32_t w[64];
-  for (int i = 0; i < 16; ++i)
-    w[i] = (uint32_t)p[4 * i] << 24 | (uint32_t)p[4 * i + 1] << 16 | (uint32_t)p[4 * i + 2] << 8 | p[4 * i + 3];
-  for (int i = 16; i < 64; ++i) {
-    const uint32_t s0 = ror(w[i - 15], 7) ^ ror(w[i - 15], 18) ^ (w[i - 15] >> 3);
-    const uint32_t s1 = ror(w[i - 2], 17) ^ ror(w[i - 2], 19) ^ (w[i - 2] >> 10);
-    w[i] = w[i - 16] + s0 + w[i - 7] + s1;
-  }
-  uint32_t a = h_[0], b = h_[1], c = h_[2], d = h_[3], e = h_[4], f = h_[5], g = h_[6], h = h_[7];
-  for (int i = 0; i < 64; ++i) {
-    const uint32_t t1 = h + (ror(e, 6) ^ ror(e, 11) ^ ror(e, 25)) + ((e & f) ^ (~e & g)) + kK[i] + w[i];
-    const uint32_t t2 = (ror(a, 2) ^ ror(a, 13) ^ ror(a, 22)) + ((a & b) ^ (a & c) ^ (b & c));
-    h = g, g = f, f = e, e = d + t1, d = c, c = b, b = a, a = t1 + t2;
-  }
-  h_[0] += a, h_[1] += b, h_[2] += c, h_[3] += d, h_[4] += e, h_[5] += f, h_[6] += g, h_[7] += h;
+// OpenSSL's SHA-256 (EVP), as the reference (src/sstable.cpp:2,22,40).
+Sha256::Sha256() : ctx_(EVP_MD_CTX_new()) {
+  if (!ctx_ || EVP_DigestInit_ex(ctx_, EVP_sha256(), nullptr) != 1) abort();
 }
 
+Sha256::~Sha256() { EVP_MD_CTX_free(ctx_); }
+
 void Sha256::Update(const void *data, size_t len) {
-  const unsigned char *p = static_cast<const unsigned char *>(data);
-  total_ += len;
-  if (used_) {
-    const size_t take = std::min(len, 64 - used_);
-    memcpy(buf_ + used_, p, take);
-    used_ += take, p += take, len -= take;
-    if (used_ < 64) return;
-    Block(buf_);
-    used_ = 0;
-  }
-  for (; len >= 64; p += 64, len -= 64) Block(p);
-  memcpy(buf_, p, len);
-  used_ = len;
+  if (EVP_DigestUpdate(ctx_, data, len) != 1) abort();
 }
 
 void Sha256::Final(unsigned char digest[32]) {
-  const uint64_t bits = total_ * 8;
-  const unsigned char pad = 0x80, zero = 0;
-  Update(&pad, 1);
-  while (used_ != 56) Update(&zero, 1);
-  unsigned char len_be[8];
-  for (int i = 0; i < 8; ++i) len_be[i] = (unsigned char)(bits >> (56 - 8 * i));
-  Update(len_be, 8);
-  for (int i = 0; i < 8; ++i)
-    for (int j = 0; j < 4; ++j) digest[4 * i + j] = (unsigned char)(h_[i] >> (24 - 8 * j));
+  unsigned int n = 0;
+  if (EVP_DigestFinal_ex(ctx_, digest, &n) != 1 || n != 32) abort();
 }
 
 string Sha256Hex(const unsigned char digest[32]) {
@@ -240,7 +195,10 @@ RC SSTableWriter::Final(unsigned char sha256_digit[32]) {
   RC rc;
   if (!data_block_.Empty() && (rc = FlushDataBlock())) return rc;
 
-  if ((rc = filter_block_.Final(buffer_))) return rc;  // the reference drops this RC
+  const auto f0 = std::chrono::steady_clock::now();
+  rc = filter_block_.Final(buffer_);  // the reference drops this RC
+  filter_seconds_ = std::chrono::duration<double>(std::chrono::steady_clock::now() - f0).count();
+  if (rc) return rc;
   if ((rc = Emit(buffer_))) return rc;
   filter_block_handle_.SetMeta(offset_, (int)buffer_.size());
   offset_ += (int)buffer_.size();

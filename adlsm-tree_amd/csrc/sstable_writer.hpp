@@ -24,6 +24,8 @@
 #include <string_view>
 #include <vector>
 
+#include <openssl/evp.h>
+
 #include "filter_block.hpp"
 #include "rc.hpp"
 
@@ -72,19 +74,18 @@ class FooterBlockWriter {
   string meta_, index_;
 };
 
-/* Incremental SHA-256 (FIPS 180-4), the file oid. */
+/* Incremental SHA-256 of the file (its oid), OpenSSL EVP like the reference. */
 class Sha256 {
  public:
   Sha256();
+  ~Sha256();
+  Sha256(const Sha256 &) = delete;
+  Sha256 &operator=(const Sha256 &) = delete;
   void Update(const void *data, size_t len);
   void Final(unsigned char digest[32]);
 
  private:
-  void Block(const unsigned char *p);
-  uint32_t h_[8];
-  unsigned char buf_[64];
-  size_t used_ = 0;
-  uint64_t total_ = 0;
+  EVP_MD_CTX *ctx_;
 };
 
 string Sha256Hex(const unsigned char digest[32]);
@@ -137,6 +138,8 @@ class SSTableWriter {
               size_t n);
   RC Final(unsigned char sha256_digit[32]);
   int GetFileSize() const { return offset_; }
+  /* wall time of the filter block build inside the last Final() */
+  double filter_seconds() const { return filter_seconds_; }
 
  private:
   RC FlushDataBlock();
@@ -151,6 +154,7 @@ class SSTableWriter {
   BlockHandle data_block_handle_, filter_block_handle_, meta_data_block_handle_, index_block_handle_;
   string last_key_;
   string buffer_;
+  double filter_seconds_ = 0;
   static constexpr size_t need_flush_size_ = 1u << 12; /* 4KB, src/sstable.hpp:40 */
 };
 
