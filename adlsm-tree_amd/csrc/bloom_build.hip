@@ -1214,7 +1214,7 @@ int adl_bloom_build(const uint8_t *h_keys, const uint64_t *h_offsets, uint64_t n
     if (!h_offsets && n && key_stride == 0) return ADL_ERR_INVALID_ARG;
     const uint64_t bytes = adl_host::bitmap_bytes(n, bits_per_key);
     if (!bytes) return bits_per_key < 0 ? ADL_ERR_INVALID_ARG : ADL_ERR_TOO_LARGE;
-    hipStream_t st = (hipStream_t)stream;
+    hipStream_t st = adl_host::sync_stream(stream);
     const uint64_t key_bytes = h_offsets ? (n ? h_offsets[n] : 0) : n * (uint64_t)key_stride;
     const uint64_t alloc = adl_host::round_up(bytes, 16);
     const uint64_t ws = adl_bloom_build_workspace_bytes(&n, 1, bits_per_key);

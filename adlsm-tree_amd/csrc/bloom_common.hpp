@@ -252,4 +252,28 @@ struct Staging {
 
 inline thread_local Staging t_stage;
 
+// The stream a synchronous host-pointer entry point runs on: the caller's, or
+// for stream == NULL a non-blocking stream of the calling thread (created on
+// first use).  The legacy null stream would order every thread's calls one
+// after the other on the device; these calls only touch their own staging
+// buffers, so nothing is lost by not ordering them with the null stream.
+struct ThreadStream {
+  hipStream_t s = nullptr;
+  bool tried = false;
+  ~ThreadStream() {
+    if (s) (void)hipStreamDestroy(s);
+  }
+  hipStream_t get() {
+    if (!tried) {
+      tried = true;
+      if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) s = nullptr;
+    }
+    return s;
+  }
+};
+
+inline thread_local ThreadStream t_stream;
+
+inline hipStream_t sync_stream(void *stream) { return stream ? (hipStream_t)stream : t_stream.get(); }
+
 }  // namespace adl_host

@@ -14,6 +14,7 @@
 // memory is DMAed directly.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -92,9 +93,18 @@ struct Pipe {
 
 thread_local Pipe t_pipe;
 
+// Wait for everything this call enqueued, ignoring errors (the error being
+// returned is the one that counts).
+void drain(Pipe &P, hipStream_t comp) {
+  if (P.up) (void)hipStreamSynchronize(P.up);
+  if (P.down) (void)hipStreamSynchronize(P.down);
+  (void)hipStreamSynchronize(comp);
+  (void)hipGetLastError();
+}
+
 struct Group {
   uint32_t f0, f1;       // filters [f0, f1)
-  uint64_t b0, b1;       // key bytes [b0, b1) uploaded (b0 16-byte aligned down)
+  uint64_t b0, b1;       // key bytes [b0, b1) uploaded (var-len: b0 16-byte aligned down)
   uint64_t k0, k1;       // keys [k0, k1)
   uint64_t off_bytes;    // offsets uploaded ((k1-k0+1)*8, var-len only)
   uint64_t out_bytes;    // device bitmap bytes (16-byte aligned per filter)
@@ -130,7 +140,11 @@ extern "C" int adl_bloom_build_segmented(const uint8_t *h_keys, const uint64_t *
       g.f1 = f1;
       g.k0 = key_begin[f0];
       g.k1 = key_begin[f1];
-      g.b0 = key_byte(g.k0) & ~15ull;
+      // var-len: offsets stay absolute, so the upload starts 16-byte aligned
+      // below the first key and the device key pointer is shifted back by b0;
+      // fixed stride: the upload starts at the group's first key exactly, so
+      // local key i sits at d_in + i * stride
+      g.b0 = h_offsets ? key_byte(g.k0) & ~15ull : key_byte(g.k0);
       g.b1 = key_byte(g.k1);
       g.off_bytes = h_offsets ? (g.k1 - g.k0 + 1) * 8 : 0;
       std::vector<uint64_t> counts;
@@ -150,7 +164,7 @@ extern "C" int adl_bloom_build_segmented(const uint8_t *h_keys, const uint64_t *
 
     Pipe &P = t_pipe;
     if (int rc = P.init()) return rc;
-    hipStream_t comp = (hipStream_t)stream;
+    hipStream_t comp = adl_host::sync_stream(stream);
     // earlier calls on this thread left nothing in flight (each call drains)
     const bool pin_in = is_pinned(h_keys) && (!h_offsets || is_pinned(h_offsets));
     const bool pin_out = is_pinned(h_bitmaps);
@@ -168,6 +182,10 @@ extern "C" int adl_bloom_build_segmented(const uint8_t *h_keys, const uint64_t *
       P.ws_cap = max_ws;
     }
     P.used_up[0] = P.used_up[1] = P.used_down[0] = P.used_down[1] = false;
+    // fault injection for the error-path tests: group g's build fails
+    // (ADL_BLOOM_FAULT_GROUP=g), with earlier groups' copies still in flight
+    const char *fault_env = getenv("ADL_BLOOM_FAULT_GROUP");
+    const long fault_group = fault_env ? atol(fault_env) : -1;
 
     std::vector<uint64_t> local_kb, dev_off;
     // host side of a finished group: copy its bitmaps out of the pinned staging
@@ -184,6 +202,7 @@ extern "C" int adl_bloom_build_segmented(const uint8_t *h_keys, const uint64_t *
       return ADL_OK;
     };
 
+    auto run = [&]() -> int {
     for (size_t gi = 0; gi < groups.size(); ++gi) {
       const Group &g = groups[gi];
       const int b = (int)(gi & 1);
@@ -220,12 +239,11 @@ extern "C" int adl_bloom_build_segmented(const uint8_t *h_keys, const uint64_t *
       }
       const uint8_t *d_keys = h_offsets ? P.d_in[b] - g.b0 : P.d_in[b];
       const uint64_t *d_offs = h_offsets ? reinterpret_cast<const uint64_t *>(P.d_in[b] + kb_al) : nullptr;
+      if ((long)gi == fault_group) return ADL_ERR_DEVICE;
       if (int rc = adl_bloom_build_segmented_device(d_keys, d_offs, key_stride, local_kb.data(), g.f1 - g.f0,
                                                     bits_per_key, P.d_out[b], dev_off.data(), P.d_ws, P.ws_cap,
-                                                    comp)) {
-        (void)hipDeviceSynchronize();
+                                                    comp))
         return rc;
-      }
       ADL_HIP_TRY(hipEventRecord(P.ev_built[b], comp));
 
       // 3. download after the build
@@ -252,6 +270,18 @@ extern "C" int adl_bloom_build_segmented(const uint8_t *h_keys, const uint64_t *
     ADL_HIP_TRY(hipStreamSynchronize(P.up));
     ADL_HIP_TRY(hipStreamSynchronize(comp));
     return ADL_OK;
+    };
+    int rc;
+    try {
+      rc = run();
+    } catch (...) {
+      rc = ADL_ERR_DEVICE;
+    }
+    // Every exit drains the three streams first, so no DMA into or out of the
+    // caller's buffers is still running once this call returns (stream syncs
+    // only: other threads' work on the device is not waited for).
+    if (rc != ADL_OK) drain(P, comp);
+    return rc;
   } catch (...) {
     return ADL_ERR_DEVICE;
   }

@@ -88,7 +88,10 @@ __global__ __launch_bounds__(kBlockP) void bloom_probe_multi_kernel(
   const bool lds_tab = nf <= kLdsFilters;
   if (lds_tab) {
     for (uint32_t f = threadIdx.x; f < nf; f += kBlockP) {
-      const FastMod fm = fastmod_for((uint32_t)(((bend ? bend[f] : boff[f + 1]) - boff[f]) * 8));
+      // an empty range (m = 0: a filter the table does not have) answers 0
+      // below and needs no divisor; fastmod_for(0) would divide by zero
+      const uint32_t m = (uint32_t)(((bend ? bend[f] : boff[f + 1]) - boff[f]) * 8);
+      const FastMod fm = m ? fastmod_for(m) : FastMod{};
       lmod[f] = ModLds{fm.magic, fm.shift};
     }
     __syncthreads();
@@ -322,7 +325,7 @@ int adl_bloom_probe(const uint8_t *h_keys, const uint64_t *h_offsets, uint64_t n
   if (n == 0) return ADL_OK;
   if (!h_keys || !h_bitmap || !h_out) return ADL_ERR_INVALID_ARG;
   if (!h_offsets && key_stride == 0) return ADL_ERR_INVALID_ARG;
-  hipStream_t st = (hipStream_t)stream;
+  hipStream_t st = adl_host::sync_stream(stream);
   const uint64_t key_bytes = h_offsets ? h_offsets[n] : n * (uint64_t)key_stride;
   const uint64_t off_bytes = h_offsets ? (n + 1) * 8 : 0;
   const uint64_t o_offs = adl_host::round_up(key_bytes + 16, 256);
@@ -376,7 +379,7 @@ int adl_bloom_murmur3(uint32_t seed, const void *data, uint64_t len, uint32_t *h
   int rc = sg.reserve(o_out + 16, o_out + 16);
   if (rc) return rc;
   if (len) memcpy(sg.host, data, len);
-  hipStream_t st = nullptr;
+  hipStream_t st = adl_host::sync_stream(nullptr);
   if (len && hipMemcpyAsync(sg.dev, sg.host, len, hipMemcpyHostToDevice, st) != hipSuccess) return ADL_ERR_DEVICE;
   hipLaunchKernelGGL(murmur3_seeded_kernel, dim3(1), dim3(kBlockP), 0, st, sg.dev, (const uint64_t *)nullptr,
                      (uint32_t)len, 1ull, seed, seed, reinterpret_cast<uint32_t *>(sg.dev + o_out));
@@ -448,8 +451,12 @@ int adl_bloom_filter_set_create(const uint8_t *h_bitmaps, const uint64_t *h_bitm
   if (!out || !h_bitmap_off || bits_per_key < 0) return ADL_ERR_INVALID_ARG;
   *out = nullptr;
   const uint64_t total = h_bitmap_off[num_filters];
-  for (uint32_t f = 0; f < num_filters; ++f)
+  for (uint32_t f = 0; f < num_filters; ++f) {
     if (h_bitmap_off[f + 1] < h_bitmap_off[f]) return ADL_ERR_INVALID_ARG;
+    // m = 8 * bytes must stay a u32 the probe can reduce by (the reference's
+    // int m, src/filter_block.cpp:50; adl_bloom_probe_device rejects the same)
+    if ((h_bitmap_off[f + 1] - h_bitmap_off[f]) * 8 > 0x7fffffffull) return ADL_ERR_TOO_LARGE;
+  }
   if (total && !h_bitmaps) return ADL_ERR_INVALID_ARG;
   auto *s = new (std::nothrow) adl_bloom_filter_set;
   if (!s) return ADL_ERR_OUT_OF_MEMORY;
@@ -479,7 +486,7 @@ int adl_bloom_filter_set_probe(const adl_bloom_filter_set *set, const uint8_t *h
   if (!set) return ADL_ERR_INVALID_ARG;
   if (n == 0) return ADL_OK;
   if (!h_keys || !h_out || (!h_offsets && key_stride == 0)) return ADL_ERR_INVALID_ARG;
-  hipStream_t st = (hipStream_t)stream;
+  hipStream_t st = adl_host::sync_stream(stream);
   const uint64_t key_bytes = h_offsets ? h_offsets[n] : n * (uint64_t)key_stride;
   const uint64_t off_bytes = h_offsets ? (n + 1) * 8 : 0;
   const uint64_t o_offs = adl_host::round_up(key_bytes + 16, 256);

@@ -7,7 +7,12 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <atomic>
+#include <map>
+#include <mutex>
+
 #include "adl_bloom.h"
+#include "filter_block_format.hpp"
 
 namespace adl {
 
@@ -78,6 +83,19 @@ RC BloomFilter::Keys2Block(const KeyArena &keys, string &result) {
   return OK;
 }
 
+RC FilterAlgorithm::Keys2Block(const KeyArena &keys, string &result) {
+  vector<string> v;
+  v.reserve(keys.size());
+  for (size_t i = 0; i < keys.size(); ++i) v.emplace_back(keys.key(i));
+  return Keys2Block(v, result);
+}
+
+RC FilterAlgorithm::IsKeysExist(const KeyArena &keys, string_view bitmap, vector<uint8_t> &out) {
+  out.assign(keys.size(), 0);
+  for (size_t i = 0; i < keys.size(); ++i) out[i] = IsKeyExists(keys.key(i), bitmap) ? 1 : 0;
+  return OK;
+}
+
 RC FilterAlgorithm::Keys2Blocks(const KeyArena &keys, const vector<uint64_t> &key_begin, string &result,
                                 vector<uint64_t> &starts) {
   starts.clear();
@@ -85,7 +103,7 @@ RC FilterAlgorithm::Keys2Blocks(const KeyArena &keys, const vector<uint64_t> &ke
     starts.push_back(result.size());
     KeyArena part;
     for (uint64_t i = key_begin[f]; i < key_begin[f + 1]; ++i)
-      part.Add(string_view(keys.bytes()).substr(keys.offsets()[i], keys.offsets()[i + 1] - keys.offsets()[i]));
+      part.Add(keys.key(i));
     if (RC rc = Keys2Block(part, result); rc != OK) return rc;
   }
   return OK;
@@ -201,38 +219,123 @@ RC FilterBlockWriter::Final(string &result) {
   return OK;
 }
 
+// ------------------------------------------------------------- FilterCache
+
+FilterCache::FilterCache(uint64_t capacity_bytes, uint32_t max_tables, int bits_per_key)
+    : bits_per_key_(bits_per_key) {
+  status_ = FromStatus(adl_bloom_filter_cache_create(capacity_bytes, max_tables, bits_per_key, &h_));
+}
+
+FilterCache::~FilterCache() { adl_bloom_filter_cache_destroy(h_); }
+
+RC FilterCache::Put(string_view oid, string_view filter_block) {
+  if (!h_) return status_;
+  return FromStatus(adl_bloom_filter_cache_put(h_, oid.data(), oid.size(),
+                                               reinterpret_cast<const uint8_t *>(filter_block.data()),
+                                               filter_block.size()));
+}
+
+bool FilterCache::Contains(string_view oid) {
+  return h_ && adl_bloom_filter_cache_contains(h_, oid.data(), oid.size()) == 1;
+}
+
+bool FilterCache::Remove(string_view oid) {
+  return h_ && adl_bloom_filter_cache_remove(h_, oid.data(), oid.size()) == 1;
+}
+
+RC FilterCache::Probe(const vector<string_view> &oids, const vector<uint32_t> &table, const KeyArena &keys,
+                      int filter, vector<uint8_t> &out, uint64_t *uncached) {
+  out.assign(keys.size(), 0);
+  if (uncached) *uncached = 0;
+  if (!h_) return status_;
+  if (table.size() != keys.size() || filter < 0) return OUT_OF_RANGE;
+  if (keys.empty()) return OK;
+  vector<const char *> ptr(oids.size());
+  vector<uint64_t> len(oids.size());
+  for (size_t j = 0; j < oids.size(); ++j) {
+    ptr[j] = oids[j].data();
+    len[j] = oids[j].size();
+  }
+  uint64_t unc = 0;
+  const int st = adl_bloom_filter_cache_probe(h_, ptr.data(), len.data(), (uint32_t)oids.size(), (uint32_t)filter,
+                                              reinterpret_cast<const uint8_t *>(keys.bytes().data()),
+                                              keys.offsets().data(), keys.size(), 0, table.data(), out.data(),
+                                              &unc, nullptr);
+  if (uncached) *uncached = unc;
+  return FromStatus(st);
+}
+
+FilterCache *FilterCache::Shared(int bits_per_key) {
+  static std::mutex mu;
+  static std::map<int, FilterCache *> *caches = new std::map<int, FilterCache *>;  // kept until exit
+  std::lock_guard<std::mutex> g(mu);
+  FilterCache *&c = (*caches)[bits_per_key];
+  if (!c) {
+    uint64_t bytes = 1ull << 30;
+    if (const char *e = getenv("ADL_BLOOM_READER_CACHE_BYTES")) bytes = strtoull(e, nullptr, 10);
+    c = new FilterCache(bytes, 1u << 20, bits_per_key);
+  }
+  return c->status() == OK ? c : nullptr;
+}
+
 // ------------------------------------------------------------- FilterBlockReader
 
 FilterBlockReader::FilterBlockReader() : filters_nums_(0), filters_offsets_offset_(0) {}
 
-FilterBlockReader::~FilterBlockReader() { adl_bloom_filter_set_destroy(device_set_); }
+FilterBlockReader::~FilterBlockReader() { Release(); }
 
-/* src/filter_block.cpp:113-155 -- same trailer walk and the same
- * FILTER_BLOCK_ERROR checks, plus bounds checks where the reference would read
- * outside the block; then the bitmaps are uploaded once (Upload). */
-RC FilterBlockReader::Init(string_view filter_blocks) {
+void FilterBlockReader::Release() {
+  if (cache_ && own_oid_) cache_->Remove(oid_);
+  cache_ = nullptr;
+  own_oid_ = false;
+  oid_.clear();
+  adl_bloom_filter_set_destroy(device_set_.exchange(nullptr));
+}
+
+/* src/filter_block.cpp:113-155 -- the trailer walk of filter_block_format.hpp
+ * (the reference's FILTER_BLOCK_ERROR checks, plus bounds checks where the
+ * reference would read outside the block). */
+RC FilterBlockReader::Parse(string_view filter_blocks) {
+  Release();
   filter_blocks_ = filter_blocks;
-  const int64_t len = (int64_t)filter_blocks_.size();
-  if (len < (int64_t)sizeof(int)) return FILTER_BLOCK_ERROR;
-  const int info_len_offset = (int)(len - sizeof(int));
-  const int info_len = Load32(&filter_blocks_[info_len_offset]);
-  if (info_len > info_len_offset || info_len <= 0) return FILTER_BLOCK_ERROR;
-  const int info_offset = info_len_offset - info_len;
-  filter_info_ = filter_blocks_.substr(info_offset, info_len);
+  filters_nums_ = 0;
+  adl_fmt::FilterBlockLayout lay;
+  if (adl_fmt::parse_filter_block(reinterpret_cast<const uint8_t *>(filter_blocks_.data()), filter_blocks_.size(),
+                                  lay))
+    return FILTER_BLOCK_ERROR;
+  filter_info_ = filter_blocks_.substr(lay.info_offset, lay.info_len);
   if (RC rc = CreateFilterAlgorithm(); rc) return rc;
-  if (info_offset < (int)sizeof(int)) return FILTER_BLOCK_ERROR;
-  const int nums_offset = info_offset - (int)sizeof(int);
-  filters_nums_ = Load32(&filter_blocks_[nums_offset]);
-  if (nums_offset < (int)sizeof(int)) return FILTER_BLOCK_ERROR;
-  filters_offsets_offset_ = Load32(&filter_blocks_[nums_offset - sizeof(int)]);
-  if (filters_offsets_offset_ < 0) return FILTER_BLOCK_ERROR;
-  if (filters_nums_ < 0 ||
-      (int64_t)filters_offsets_offset_ + (int64_t)sizeof(int) * (filters_nums_ ? filters_nums_ : 1) >
-          nums_offset)
-    return FILTER_BLOCK_ERROR; /* the reference reads out of bounds here */
-  if (Load32(&filter_blocks_[filters_offsets_offset_]) != 0) return FILTER_BLOCK_ERROR;
+  filters_nums_ = lay.num_filters;
+  filters_offsets_offset_ = lay.offsets_start;
   filters_offsets_ = filter_blocks_.substr(filters_offsets_offset_, sizeof(int) * filters_nums_);
-  return Upload();
+  return OK;
+}
+
+RC FilterBlockReader::Init(string_view filter_blocks) {
+  if (RC rc = Parse(filter_blocks); rc) return rc;
+  FilterCache *c = FilterCache::Shared(bits_per_key_);
+  if (!c) return DEVICE_ERROR;
+  static std::atomic<uint64_t> next_id{0};
+  oid_ = "\x01reader:" + std::to_string(next_id.fetch_add(1));
+  const RC rc = c->Put(oid_, filter_blocks_);
+  if (rc == OK) {
+    cache_ = c;
+    own_oid_ = true;
+    return OK;
+  }
+  oid_.clear();
+  if (rc == FILTER_BLOCK_ERROR) return rc;
+  return Upload();  // larger than the shared arena: a device copy of its own
+}
+
+RC FilterBlockReader::Init(string_view filter_blocks, FilterCache &cache, string_view oid) {
+  if (RC rc = Parse(filter_blocks); rc) return rc;
+  if (cache.bits_per_key() != bits_per_key_) return FILTER_BLOCK_ERROR;
+  oid_.assign(oid.data(), oid.size());
+  cache_ = &cache;
+  own_oid_ = false;
+  if (cache.Contains(oid_)) return OK;  // another reader of this SSTable uploaded it
+  return cache.Put(oid_, filter_blocks_);
 }
 
 /* src/filter_block.cpp:158-170 -- only "bf" is known; bits_per_key at info[3]. */
@@ -245,46 +348,60 @@ RC FilterBlockReader::CreateFilterAlgorithm() {
 }
 
 RC FilterBlockReader::Upload() {
-  adl_bloom_filter_set_destroy(device_set_);
-  device_set_ = nullptr;
   vector<uint64_t> off(filters_nums_ + 1);
-  for (int i = 0; i < filters_nums_; ++i) {
-    const int o = Load32(&filters_offsets_[i * sizeof(int)]);
-    if (o < 0 || o > filters_offsets_offset_ || (i && (uint64_t)o < off[i - 1])) return FILTER_BLOCK_ERROR;
-    off[i] = (uint64_t)o;
-  }
+  for (int i = 0; i < filters_nums_; ++i) off[i] = (uint64_t)Load32(&filters_offsets_[i * sizeof(int)]);
   off[filters_nums_] = (uint64_t)filters_offsets_offset_;
+  adl_bloom_filter_set *set = nullptr;
   const int st = adl_bloom_filter_set_create(reinterpret_cast<const uint8_t *>(filter_blocks_.data()),
-                                             off.data(), (uint32_t)filters_nums_, bits_per_key_,
-                                             &device_set_);
+                                             off.data(), (uint32_t)filters_nums_, bits_per_key_, &set);
+  if (st == ADL_OK) device_set_.store(set);
   return FromStatus(st);
+}
+
+/* One launch over the batch.  The cache may have evicted this block (other
+ * tables took its room): then it is uploaded again from the reader's view
+ * and the probe repeated.  A block that keeps being evicted before its probe
+ * runs (a cache far too small for its working set) moves to a device copy
+ * of the reader's own, so the answers stay exact. */
+RC FilterBlockReader::Probe(int filter_block_num, const KeyArena &keys, vector<uint8_t> &out) {
+  if (!device_set_ && cache_) {
+    const vector<string_view> oids{oid_};
+    const vector<uint32_t> table(keys.size(), 0);
+    for (int attempt = 0; attempt < 4; ++attempt) {
+      uint64_t uncached = 0;
+      if (RC rc = cache_->Probe(oids, table, keys, filter_block_num, out, &uncached); rc) return rc;
+      if (uncached == 0) return OK;
+      if (RC rc = cache_->Put(oid_, filter_blocks_); rc) return rc;
+    }
+    std::lock_guard<std::mutex> g(upload_mu_);
+    if (!device_set_)
+      if (RC rc = Upload(); rc) return rc;
+  }
+  if (!device_set_) return FILTER_BLOCK_ERROR;
+  out.assign(keys.size(), 0);
+  return FromStatus(adl_bloom_filter_set_probe(device_set_.load(), reinterpret_cast<const uint8_t *>(keys.bytes().data()),
+                                               keys.offsets().data(), keys.size(), 0, nullptr,
+                                               (uint32_t)filter_block_num, out.data(), nullptr));
 }
 
 /* src/filter_block.cpp:172-184 -- one key against filter `filter_block_num`.
  * A device failure answers true ("may be present"). */
 bool FilterBlockReader::IsKeyExists(int filter_block_num, string_view key) {
-  if (filter_block_num < 0 || filter_block_num >= filters_nums_ || !device_set_) return false;
-  const uint64_t offs[2] = {0, key.size()};
-  const char empty = 0;
-  uint8_t hit = 1;
-  const int st = adl_bloom_filter_set_probe(
-      device_set_, reinterpret_cast<const uint8_t *>(key.empty() ? &empty : key.data()), offs, 1, 0,
-      nullptr, (uint32_t)filter_block_num, &hit, nullptr);
-  if (st != ADL_OK) {
-    fprintf(stderr, "adl::FilterBlockReader::IsKeyExists: %s\n", adl_bloom_strerror(st));
+  if (filter_block_num < 0 || filter_block_num >= filters_nums_) return false;
+  KeyArena one;
+  one.Add(key);
+  vector<uint8_t> hit;
+  if (RC rc = Probe(filter_block_num, one, hit); rc) {
+    fprintf(stderr, "adl::FilterBlockReader::IsKeyExists: %s\n", string(strrc(rc)).c_str());
     return true;
   }
-  return hit != 0;
+  return hit[0] != 0;
 }
 
 RC FilterBlockReader::IsKeysExist(int filter_block_num, const KeyArena &keys, vector<uint8_t> &out) {
   out.assign(keys.size(), 0);
   if (filter_block_num < 0 || filter_block_num >= filters_nums_ || keys.empty()) return OK;
-  if (!device_set_) return FILTER_BLOCK_ERROR;
-  const int st = adl_bloom_filter_set_probe(
-      device_set_, reinterpret_cast<const uint8_t *>(keys.bytes().data()), keys.offsets().data(),
-      keys.size(), 0, nullptr, (uint32_t)filter_block_num, out.data(), nullptr);
-  return FromStatus(st);
+  return Probe(filter_block_num, keys, out);
 }
 
 /* src/murmur3_hash.cpp:11-65, evaluated on the GPU.  There is no error channel

@@ -11,13 +11,16 @@
 //     build (adl_bloom_build_segmented) straight into the block buffer, at the
 //     byte offsets the reference's successive appends would give them.
 //   * FilterBlockReader::Init uploads the block's bitmaps once into a
-//     device-resident filter set; IsKeyExists probes on the GPU.  Batched
-//     IsKeysExist() is the intended read path (one launch per batch).
+//     FilterCache arena (keyed by SSTable oid); IsKeyExists probes on the GPU.
+//     Batched IsKeysExist() and the level multi-get (level_filter.hpp) are
+//     the intended read paths (one launch per batch).
 //   * Device failures surface as RC::DEVICE_ERROR; nothing throws.
 #pragma once
 #include <stdint.h>
 
+#include <atomic>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <string_view>
 #include <vector>
@@ -25,6 +28,7 @@
 #include "rc.hpp"
 
 struct adl_bloom_filter_set;
+struct adl_bloom_filter_cache;
 
 namespace adl {
 
@@ -43,6 +47,9 @@ class KeyArena {
     offsets_.assign(1, 0);
   }
   size_t size() const { return offsets_.size() - 1; }
+  string_view key(size_t i) const {
+    return string_view(bytes_).substr(offsets_[i], offsets_[i + 1] - offsets_[i]);
+  }
   bool empty() const { return size() == 0; }
   const string &bytes() const { return bytes_; }
   const vector<uint64_t> &offsets() const { return offsets_; }
@@ -52,21 +59,27 @@ class KeyArena {
   vector<uint64_t> offsets_;
 };
 
-/* src/filter_block.hpp:13-20 */
+/* src/filter_block.hpp:13-20.  The first three members are the reference's;
+ * the batched extensions after them have default implementations in terms of
+ * those three, so a subclass written against the reference's FilterAlgorithm
+ * (overriding only Keys2Block(vector<string>), IsKeyExists and FilterInfo)
+ * compiles and works unchanged in FilterBlockWriter / FilterBlockReader.
+ * BloomFilter overrides them with the batched GPU path. */
 class FilterAlgorithm {
  public:
   virtual RC Keys2Block(const vector<string> &keys, string &result) = 0;
   virtual bool IsKeyExists(string_view key, string_view bitmap) = 0;
   virtual void FilterInfo(string &/*info*/) { /* NOTHING */ }
-  /* batched extensions */
-  virtual RC Keys2Block(const KeyArena &keys, string &result) = 0;
+  /* batched extensions (defaults: unpack and call the reference methods) */
+  virtual RC Keys2Block(const KeyArena &keys, string &result);
   /* Keys2Block for consecutive filters: filter f = keys [key_begin[f],
    * key_begin[f+1]); the bitmaps are appended to result back to back, as
    * successive Keys2Block calls would, filter f starting at starts[f].  The
    * default loops over Keys2Block. */
   virtual RC Keys2Blocks(const KeyArena &keys, const vector<uint64_t> &key_begin, string &result,
                          vector<uint64_t> &starts);
-  virtual RC IsKeysExist(const KeyArena &keys, string_view bitmap, vector<uint8_t> &out) = 0;
+  /* out[i] = IsKeyExists(key i, bitmap); the default loops over IsKeyExists */
+  virtual RC IsKeysExist(const KeyArena &keys, string_view bitmap, vector<uint8_t> &out);
   virtual ~FilterAlgorithm() = default;
 };
 
@@ -105,22 +118,66 @@ class FilterBlockWriter {
   unique_ptr<FilterAlgorithm> method_;
 };
 
-/* src/filter_block.hpp:54-73 */
+/* Device-resident filter blocks of many SSTables in one HBM arena, keyed by
+ * oid (the SSTable's SHA-256 file name), least recently used evicted first:
+ * the filter side of DB::table_cache_ (src/db.hpp:96-97, LRUCache
+ * src/cache.hpp:23-93).  C++ handle over adl_bloom_filter_cache (C-ABI);
+ * thread-safe, and no lock is held while a probe runs on the device. */
+class FilterCache {
+ public:
+  FilterCache(uint64_t capacity_bytes, uint32_t max_tables, int bits_per_key);
+  ~FilterCache();
+  FilterCache(const FilterCache &) = delete;
+  FilterCache &operator=(const FilterCache &) = delete;
+  RC status() const { return status_; } /* creation result */
+  int bits_per_key() const { return bits_per_key_; }
+  /* FilterBlockReader::Init's checks (FILTER_BLOCK_ERROR), then one upload */
+  RC Put(string_view oid, string_view filter_block);
+  bool Contains(string_view oid);
+  bool Remove(string_view oid);
+  /* One launch for the batch: out[i] = filter `filter` of table
+   * oids[table[i]] may contain keys[i] (a table that is not cached answers 1,
+   * "may be present"; *uncached counts those queries). */
+  RC Probe(const vector<string_view> &oids, const vector<uint32_t> &table, const KeyArena &keys, int filter,
+           vector<uint8_t> &out, uint64_t *uncached = nullptr);
+  /* The process-wide cache FilterBlockReader::Init(string_view) keeps its
+   * bitmaps in, one per bits_per_key (arena ADL_BLOOM_READER_CACHE_BYTES,
+   * default 1 GiB); created on first use and kept until exit. */
+  static FilterCache *Shared(int bits_per_key);
+
+ private:
+  adl_bloom_filter_cache *h_ = nullptr;
+  int bits_per_key_;
+  RC status_;
+};
+
+/* src/filter_block.hpp:54-73.  The bitmaps live in a FilterCache arena (one
+ * upload per block, no allocation per Init); the reader keeps the caller's
+ * view of the block, as the reference's does, and re-uploads it if the cache
+ * evicted it. */
 class FilterBlockReader {
  public:
   FilterBlockReader();
   ~FilterBlockReader();
   FilterBlockReader(const FilterBlockReader &) = delete;
   FilterBlockReader &operator=(const FilterBlockReader &) = delete;
+  /* src/filter_block.hpp:57: the bitmaps go into FilterCache::Shared(bpk)
+   * under an id private to this reader (removed by the destructor) */
   RC Init(string_view filter_block);
+  /* the same, with the table's entry in `cache` under `oid`: every reader of
+   * one SSTable (and a level multi-get over it) shares one device copy */
+  RC Init(string_view filter_block, FilterCache &cache, string_view oid);
   bool IsKeyExists(int filter_block_num, string_view key);
-  /* batched: out[i] = IsKeyExists(filter_block_num, key i) */
+  /* batched: out[i] = IsKeyExists(filter_block_num, key i), one launch */
   RC IsKeysExist(int filter_block_num, const KeyArena &keys, vector<uint8_t> &out);
   int filters_nums() const { return filters_nums_; }
 
  private:
+  RC Parse(string_view filter_block);
   RC CreateFilterAlgorithm();
   RC Upload();
+  RC Probe(int filter_block_num, const KeyArena &keys, vector<uint8_t> &out);
+  void Release();
 
   int filters_nums_;
   int filters_offsets_offset_;
@@ -129,7 +186,12 @@ class FilterBlockReader {
   string_view filter_blocks_;
   unique_ptr<FilterAlgorithm> method_;
   int bits_per_key_ = 0;
-  adl_bloom_filter_set *device_set_ = nullptr; /* owned device copy of the bitmaps */
+  FilterCache *cache_ = nullptr;               /* where the bitmaps are resident */
+  string oid_;                                 /* their key in cache_ */
+  bool own_oid_ = false;                       /* a private id: removed with the reader */
+  std::mutex upload_mu_;                       /* guards the move to device_set_ */
+  std::atomic<adl_bloom_filter_set *> device_set_{nullptr}; /* a copy of its own: blocks larger than
+                                                   the shared arena, or evicted again and again */
 };
 
 /* src/murmur3_hash.hpp:9 -- computed on the GPU (adl_bloom_murmur3). */

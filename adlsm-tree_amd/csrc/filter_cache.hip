@@ -20,12 +20,22 @@
 //    cached answers 1 ("may be present": the caller reads the table), one
 //    bound for a filter the block does not have answers 0, as
 //    FilterBlockReader::IsKeyExists does (src/filter_block.cpp:174).
-//  * One mutex per cache: put/remove/probe are serialised, and a probe holds
-//    it until its kernel is done, so no block is evicted under a running probe.
+//  * Concurrency: one mutex per cache guards the index, the LRU list and the
+//    arena's free list, and is held only for that bookkeeping -- never across
+//    a copy or a kernel.  A probe pins the entries it resolved (a count per
+//    entry) before it lets go of the lock; an entry evicted, replaced or
+//    removed while pinned leaves the index at once but keeps its arena range
+//    until the last probe using it unpins it.  A put reserves its range under
+//    the lock, uploads without it, and publishes under it again; a put that
+//    finds no room while pinned or uploading blocks hold the arena waits for
+//    them (condition variable) instead of failing.  So probes never wait for
+//    each other, and readers, like the reference's (src/db.cpp:166-172), take
+//    no lock for the duration of a lookup.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string.h>
 
+#include <condition_variable>
 #include <list>
 #include <map>
 #include <mutex>
@@ -34,64 +44,46 @@
 #include <vector>
 
 #include "bloom_common.hpp"
+#include "filter_block_format.hpp"
 
 namespace {
 
 constexpr uint64_t kAlign = 256;
 constexpr uint64_t kOnesBytes = 16;  // an all-ones 16-byte filter: every probe hits
 
-int32_t load32(const uint8_t *p) {
-  int32_t v;
-  memcpy(&v, p, 4);
-  return v;
-}
-
-// FilterBlockReader::Init's trailer walk (src/filter_block.cpp:113-155):
-// bitmaps region [0, offsets_start), filter f = [off_f, off_{f+1} or offsets_start).
+// FilterBlockReader::Init's trailer walk (src/filter_block.cpp:113-155, in
+// filter_block_format.hpp): bitmaps region [0, offsets_start), filter f =
+// [off_f, off_{f+1} or offsets_start); one bits_per_key (so one k) per cache.
 int parse_block(const uint8_t *b, uint64_t len, int32_t want_bpk, std::vector<uint64_t> &off) {
-  if (len < 4 || len > 0x7fffffffull) return ADL_FILTER_BLOCK_ERROR;
-  const int64_t info_len_offset = (int64_t)len - 4;
-  const int32_t info_len = load32(b + info_len_offset);
-  if (info_len <= 0 || info_len > info_len_offset) return ADL_FILTER_BLOCK_ERROR;
-  const int64_t info_offset = info_len_offset - info_len;
-  // CreateFilterAlgorithm (:158-170): "bf" and bits_per_key at info[3]
-  if (info_len < 7 || b[info_offset] != 'b' || b[info_offset + 1] != 'f') return ADL_FILTER_BLOCK_ERROR;
-  const int32_t bpk = load32(b + info_offset + 3);
-  if (bpk != want_bpk) return ADL_ERR_INVALID_ARG;  // one k per cache
-  if (info_offset < 4) return ADL_FILTER_BLOCK_ERROR;
-  const int64_t nums_offset = info_offset - 4;
-  const int32_t nf = load32(b + nums_offset);
-  if (nums_offset < 4) return ADL_FILTER_BLOCK_ERROR;
-  const int32_t offsets_start = load32(b + nums_offset - 4);
-  if (offsets_start < 0 || nf < 0) return ADL_FILTER_BLOCK_ERROR;
-  if ((int64_t)offsets_start + 4ll * (nf ? nf : 1) > nums_offset) return ADL_FILTER_BLOCK_ERROR;
-  if (load32(b + offsets_start) != 0) return ADL_FILTER_BLOCK_ERROR;
-  off.assign((size_t)nf + 1, 0);
-  for (int32_t f = 0; f < nf; ++f) {
-    const int32_t o = load32(b + offsets_start + 4ll * f);
-    if (o < 0 || o > offsets_start || (f && (uint64_t)o < off[f - 1])) return ADL_FILTER_BLOCK_ERROR;
-    off[f] = (uint64_t)o;
-  }
-  off[nf] = (uint64_t)offsets_start;
+  adl_fmt::FilterBlockLayout lay;
+  if (adl_fmt::parse_filter_block(b, len, lay)) return ADL_FILTER_BLOCK_ERROR;
+  if (lay.bits_per_key != want_bpk) return ADL_ERR_INVALID_ARG;
+  off = std::move(lay.off);
   return ADL_OK;
 }
 
 }  // namespace
 
 struct adl_bloom_filter_cache {
+  enum State : uint8_t { kLive, kLoading, kDead };
   struct Entry {
     std::string oid;
     uint64_t base = 0, size = 0;  // arena range [base, base + size)
     std::vector<uint64_t> off;    // block-relative filter offsets (F+1)
+    uint32_t pins = 0;            // probes (or the uploading put) using the range
+    State state = kLive;
   };
+  using Iter = std::list<Entry>::iterator;
   std::mutex mu;
-  uint8_t *arena = nullptr;  // [ones][blocks...]
+  std::condition_variable freed;  // a dead or loading entry gave back its range
+  uint8_t *arena = nullptr;       // [ones][blocks...]
   uint64_t capacity = 0, used = 0;
   uint32_t max_tables = 0;
   int32_t bpk = 0;
-  std::list<Entry> lru;  // front = most recently used
-  std::unordered_map<std::string, std::list<Entry>::iterator> index;
-  std::map<uint64_t, uint64_t> free_;  // offset -> size, coalesced
+  std::list<Entry> lru;      // live entries, front = most recently used
+  std::list<Entry> limbo;    // loading (pinned by their put) and dead (pinned by probes)
+  std::unordered_map<std::string, Iter> index;  // live entries only
+  std::map<uint64_t, uint64_t> free_;           // offset -> size, coalesced
 
   bool alloc(uint64_t size, uint64_t &at) {
     for (auto it = free_.begin(); it != free_.end(); ++it) {
@@ -121,11 +113,25 @@ struct adl_bloom_filter_cache {
       }
     }
   }
-  void evict_back() {
-    Entry &e = lru.back();
-    release(e.base, e.size);
-    index.erase(e.oid);
-    lru.pop_back();
+  // Take a live entry out of the index: its range is freed now, or -- while
+  // probes hold it -- by the last of them (unpin).
+  void retire(Iter it) {
+    index.erase(it->oid);
+    if (it->pins == 0) {
+      release(it->base, it->size);
+      lru.erase(it);
+      freed.notify_all();
+    } else {
+      it->state = kDead;
+      limbo.splice(limbo.end(), lru, it);
+    }
+  }
+  void unpin(Iter it) {
+    if (--it->pins == 0 && it->state == kDead) {
+      release(it->base, it->size);
+      limbo.erase(it);
+      freed.notify_all();
+    }
   }
 };
 
@@ -141,10 +147,12 @@ int adl_bloom_filter_cache_create(uint64_t capacity_bytes, uint32_t max_tables, 
     c->max_tables = max_tables;
     c->bpk = bits_per_key;
     if (hipMalloc((void **)&c->arena, c->capacity + kAlign) != hipSuccess) {
+      (void)hipGetLastError();
       delete c;
       return ADL_ERR_OUT_OF_MEMORY;
     }
-    if (hipMemset(c->arena, 0xff, kOnesBytes) != hipSuccess) {
+    hipStream_t st = adl_host::sync_stream(nullptr);
+    if (hipMemsetAsync(c->arena, 0xff, kOnesBytes, st) != hipSuccess || hipStreamSynchronize(st) != hipSuccess) {
       (void)hipFree(c->arena);
       delete c;
       return ADL_ERR_DEVICE;
@@ -157,6 +165,7 @@ int adl_bloom_filter_cache_create(uint64_t capacity_bytes, uint32_t max_tables, 
   }
 }
 
+// No call on the cache may be running or start once this is called.
 int adl_bloom_filter_cache_destroy(adl_bloom_filter_cache *c) {
   if (!c) return ADL_OK;
   (void)hipFree(c->arena);
@@ -172,26 +181,55 @@ int adl_bloom_filter_cache_put(adl_bloom_filter_cache *c, const char *oid, uint6
     if (int rc = parse_block(h_block, block_len, c->bpk, off)) return rc;
     const uint64_t bytes = off.back();  // the bitmap region
     const uint64_t size = adl_host::round_up(bytes + 1, kAlign);
-    std::lock_guard<std::mutex> g(c->mu);
-    if (size > c->capacity) return ADL_ERR_OUT_OF_MEMORY;
     const std::string key(oid, oid_len);
-    if (auto it = c->index.find(key); it != c->index.end()) {  // replace, as LRUCache::Put does
-      c->release(it->second->base, it->second->size);
-      c->lru.erase(it->second);
-      c->index.erase(it);
+    adl_bloom_filter_cache::Iter mine;
+    {
+      std::unique_lock<std::mutex> g(c->mu);
+      if (size > c->capacity) return ADL_ERR_OUT_OF_MEMORY;
+      // 1. room: the table count (LRUCache's maxSize) and the arena bytes.  A
+      //    block being replaced (LRUCache::Put of a cached key) stays visible to
+      //    probes until the new one is published.
+      const size_t replacing = c->index.count(key);
+      while (c->lru.size() - replacing >= c->max_tables) c->retire(std::prev(c->lru.end()));
+      uint64_t at = 0;
+      while (!c->alloc(size, at)) {
+        if (!c->lru.empty()) {
+          c->retire(std::prev(c->lru.end()));
+        } else if (!c->limbo.empty()) {
+          c->freed.wait(g);  // pinned or uploading blocks hold the rest of the arena
+        } else {
+          return ADL_ERR_OUT_OF_MEMORY;  // cannot happen: an empty arena fits any size <= capacity
+        }
+      }
+      // 2. reserve the range, pinned by this put while it uploads
+      adl_bloom_filter_cache::Entry e;
+      e.oid = key;
+      e.base = at;
+      e.size = size;
+      e.off = std::move(off);
+      e.pins = 1;
+      e.state = adl_bloom_filter_cache::kLoading;
+      mine = c->limbo.insert(c->limbo.end(), std::move(e));
     }
-    while (c->lru.size() >= c->max_tables) c->evict_back();
-    uint64_t at = 0;
-    while (!c->alloc(size, at)) {
-      if (c->lru.empty()) return ADL_ERR_OUT_OF_MEMORY;  // fragmentation: cannot happen once empty
-      c->evict_back();
-    }
-    if (bytes && hipMemcpy(c->arena + at, h_block, bytes, hipMemcpyHostToDevice) != hipSuccess) {
-      c->release(at, size);
+    // 3. upload without the lock
+    hipStream_t st = adl_host::sync_stream(nullptr);
+    const bool ok = !bytes || (hipMemcpyAsync(c->arena + mine->base, h_block, bytes, hipMemcpyHostToDevice, st) ==
+                                   hipSuccess &&
+                               hipStreamSynchronize(st) == hipSuccess);
+    // 4. publish as most recently used (or give the range back)
+    std::lock_guard<std::mutex> g(c->mu);
+    if (!ok) {
+      mine->state = adl_bloom_filter_cache::kDead;
+      c->unpin(mine);
       return ADL_ERR_DEVICE;
     }
-    c->lru.push_front(adl_bloom_filter_cache::Entry{key, at, size, std::move(off)});
+    if (auto it = c->index.find(key); it != c->index.end()) c->retire(it->second);  // the block this one replaces
+    mine->pins = 0;
+    mine->state = adl_bloom_filter_cache::kLive;
+    c->lru.splice(c->lru.begin(), c->limbo, mine);
     c->index[key] = c->lru.begin();
+    while (c->lru.size() > c->max_tables) c->retire(std::prev(c->lru.end()));
+    c->freed.notify_all();  // a put waiting for room may evict this entry now
     return ADL_OK;
   } catch (...) {
     return ADL_ERR_OUT_OF_MEMORY;
@@ -212,9 +250,7 @@ int adl_bloom_filter_cache_remove(adl_bloom_filter_cache *c, const char *oid, ui
   std::lock_guard<std::mutex> g(c->mu);
   auto it = c->index.find(std::string(oid, oid_len));
   if (it == c->index.end()) return 0;
-  c->release(it->second->base, it->second->size);
-  c->lru.erase(it->second);
-  c->index.erase(it);
+  c->retire(it->second);
   return 1;
 }
 
@@ -235,36 +271,46 @@ int adl_bloom_filter_cache_probe(adl_bloom_filter_cache *c, const char *const *o
   if (n == 0) return ADL_OK;
   if (!h_keys || !h_table || !h_out || (!h_offsets && key_stride == 0)) return ADL_ERR_INVALID_ARG;
   try {
-    hipStream_t st = (hipStream_t)stream;
-    std::lock_guard<std::mutex> g(c->mu);
-    // per listed table: the arena range of its filter `filter` (the all-ones
-    // filter when the table is not cached, an empty range when it has no
-    // such filter)
+    for (uint64_t i = 0; i < n; ++i)
+      if (h_table[i] >= num_tables) return ADL_ERR_INVALID_ARG;
+    hipStream_t st = adl_host::sync_stream(stream);
+    // 1. under the lock: per listed table, the arena range of its filter
+    //    `filter` (the all-ones filter when the table is not cached, an empty
+    //    range when it has no such filter), its entry pinned and marked used
     std::vector<uint64_t> be(2 * (size_t)num_tables);
     std::vector<uint8_t> cached(num_tables);
-    for (uint32_t j = 0; j < num_tables; ++j) {
-      auto it = c->index.find(std::string(oids[j], oid_lens[j]));
-      if (it == c->index.end()) {
-        be[j] = 0;
-        be[num_tables + j] = kOnesBytes;
-        continue;
-      }
-      cached[j] = 1;
-      c->lru.splice(c->lru.begin(), c->lru, it->second);
-      const adl_bloom_filter_cache::Entry &e = *it->second;
-      const uint64_t nf = e.off.size() - 1;
-      be[j] = be[num_tables + j] = e.base;
-      if (filter < nf) {
-        be[j] = e.base + e.off[filter];
-        be[num_tables + j] = e.base + e.off[filter + 1];
+    std::vector<adl_bloom_filter_cache::Iter> pinned;
+    pinned.reserve(num_tables);
+    {
+      std::lock_guard<std::mutex> g(c->mu);
+      for (uint32_t j = 0; j < num_tables; ++j) {
+        auto it = c->index.find(std::string(oids[j], oid_lens[j]));
+        if (it == c->index.end()) {
+          be[j] = 0;
+          be[num_tables + j] = kOnesBytes;
+          continue;
+        }
+        cached[j] = 1;
+        adl_bloom_filter_cache::Iter e = it->second;
+        c->lru.splice(c->lru.begin(), c->lru, e);
+        ++e->pins;
+        pinned.push_back(e);
+        const uint64_t nf = e->off.size() - 1;
+        be[j] = be[num_tables + j] = e->base;
+        if (filter < nf) {
+          be[j] = e->base + e->off[filter];
+          be[num_tables + j] = e->base + e->off[filter + 1];
+        }
       }
     }
+    auto unpin_all = [&] {
+      std::lock_guard<std::mutex> g(c->mu);
+      for (auto e : pinned) c->unpin(e);
+    };
     uint64_t uncached = 0;
-    for (uint64_t i = 0; i < n; ++i) {
-      if (h_table[i] >= num_tables) return ADL_ERR_INVALID_ARG;
-      uncached += !cached[h_table[i]];
-    }
-    // stage keys, offsets, table ids and the range table in one H2D
+    for (uint64_t i = 0; i < n; ++i) uncached += !cached[h_table[i]];
+    // 2. without the lock: stage keys, offsets, table ids and the range table
+    //    in one H2D, one probe launch, one D2H
     const uint64_t key_bytes = h_offsets ? h_offsets[n] : n * (uint64_t)key_stride;
     const uint64_t off_bytes = h_offsets ? (n + 1) * 8 : 0;
     const uint64_t o_offs = adl_host::round_up(key_bytes + 16, 256);
@@ -273,24 +319,27 @@ int adl_bloom_filter_cache_probe(adl_bloom_filter_cache *c, const char *const *o
     const uint64_t o_out = o_be + adl_host::round_up(be.size() * 8, 256);
     const uint64_t total = o_out + adl_host::round_up(n, 256);
     adl_host::Staging &sg = adl_host::t_stage;
-    if (int rc = sg.reserve(o_out, total)) return rc;
-    if (key_bytes) memcpy(sg.host, h_keys, key_bytes);
-    if (off_bytes) memcpy(sg.host + o_offs, h_offsets, off_bytes);
-    memcpy(sg.host + o_fid, h_table, n * 4);
-    memcpy(sg.host + o_be, be.data(), be.size() * 8);
-    if (hipMemcpyAsync(sg.dev, sg.host, o_out, hipMemcpyHostToDevice, st) != hipSuccess) return ADL_ERR_DEVICE;
-    const uint64_t *d_be = reinterpret_cast<const uint64_t *>(sg.dev + o_be);
-    int rc = adl_bloom_probe_ranges_device(sg.dev, h_offsets ? reinterpret_cast<uint64_t *>(sg.dev + o_offs) : nullptr,
-                                           n, key_stride, reinterpret_cast<const uint32_t *>(sg.dev + o_fid),
-                                           num_tables, c->arena, d_be, d_be + num_tables, c->bpk, sg.dev + o_out,
-                                           stream);
-    if (rc) {
-      (void)hipStreamSynchronize(st);
-      return rc;
+    int rc = sg.reserve(o_out, total);
+    if (rc == ADL_OK) {
+      if (key_bytes) memcpy(sg.host, h_keys, key_bytes);
+      if (off_bytes) memcpy(sg.host + o_offs, h_offsets, off_bytes);
+      memcpy(sg.host + o_fid, h_table, n * 4);
+      memcpy(sg.host + o_be, be.data(), be.size() * 8);
+      if (hipMemcpyAsync(sg.dev, sg.host, o_out, hipMemcpyHostToDevice, st) != hipSuccess) rc = ADL_ERR_DEVICE;
     }
-    if (hipMemcpyAsync(sg.host, sg.dev + o_out, n, hipMemcpyDeviceToHost, st) != hipSuccess ||
-        hipStreamSynchronize(st) != hipSuccess)
-      return ADL_ERR_DEVICE;
+    if (rc == ADL_OK) {
+      const uint64_t *d_be = reinterpret_cast<const uint64_t *>(sg.dev + o_be);
+      rc = adl_bloom_probe_ranges_device(sg.dev, h_offsets ? reinterpret_cast<uint64_t *>(sg.dev + o_offs) : nullptr,
+                                         n, key_stride, reinterpret_cast<const uint32_t *>(sg.dev + o_fid),
+                                         num_tables, c->arena, d_be, d_be + num_tables, c->bpk, sg.dev + o_out, st);
+    }
+    if (rc == ADL_OK && hipMemcpyAsync(sg.host, sg.dev + o_out, n, hipMemcpyDeviceToHost, st) != hipSuccess)
+      rc = ADL_ERR_DEVICE;
+    // the kernel and the copies are done before any pinned range can be reused
+    if (hipStreamSynchronize(st) != hipSuccess && rc == ADL_OK) rc = ADL_ERR_DEVICE;
+    // 3. unpin (a range retired meanwhile is freed by its last unpin)
+    unpin_all();
+    if (rc) return rc;
     memcpy(h_out, sg.host, n);
     if (h_uncached) *h_uncached = uncached;
     return ADL_OK;

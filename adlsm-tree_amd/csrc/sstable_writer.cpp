@@ -149,6 +149,9 @@ RC PosixFileSink::Finish(string_view oid_hex) {
 SSTableWriter::SSTableWriter(Sink *sink, int bits_per_key)
     : sink_(sink), filter_block_(make_unique<BloomFilter>(bits_per_key)) {}
 
+SSTableWriter::SSTableWriter(Sink *sink, unique_ptr<FilterAlgorithm> &&filter)
+    : sink_(sink), filter_block_(std::move(filter)) {}
+
 /* src/sstable.cpp:26-35: the user key (inner key minus seq and op,
  * src/keys.cpp:7-9) goes to the filter, the entry to the data block. */
 RC SSTableWriter::Add(string_view inner_key, string_view value) {

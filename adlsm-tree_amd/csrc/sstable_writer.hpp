@@ -130,6 +130,9 @@ class PosixFileSink : public Sink {
 class SSTableWriter {
  public:
   SSTableWriter(Sink *sink, int bits_per_key = 10);
+  /* any FilterAlgorithm (src/filter_block.hpp:13-20), e.g. one written
+   * against the reference's interface */
+  SSTableWriter(Sink *sink, unique_ptr<FilterAlgorithm> &&filter);
   /* inner_key = user_key + LE64 seq + op byte (src/keys.cpp:76-84) */
   RC Add(string_view inner_key, string_view value);
   /* entries i = [key_off[i], key_off[i+1]) of keys, [val_off[i], val_off[i+1])

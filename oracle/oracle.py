@@ -277,3 +277,42 @@ class FilterBlockReaderOracle:
         o1, o2 = self.filter_range(i)
         bm = np.frombuffer(self.block[o1:o2], dtype=np.uint8)
         return bool(probe([bytes(key)], bm, bits_per_key=self.bits_per_key)[0])
+
+
+# ---------------------------------------------------------------- level lookup
+def _decode_inner(k: bytes):
+    """MemKey::FromKey (src/keys.cpp:86-91): user key, int64 seq, op byte."""
+    if len(k) < 9:
+        return k, 0, 0
+    return k[:-9], struct.unpack("<q", k[-9:-1])[0], k[-1]
+
+
+def _memkey_less(a, b) -> bool:
+    """MemKey::operator< (src/keys.cpp:61-74)."""
+    if a[0] != b[0]:
+        return a[0] < b[0]
+    if a[1] != b[1]:
+        return a[1] > b[1]
+    return a[2] > b[2]
+
+
+def level_candidates(tables, user_key: bytes, seq: int):
+    """Level::Get's visiting order and range test (src/revision.cpp:278-287):
+    files_meta_ ordered by min_inner_key (src/file_util.hpp:163-165), walked in
+    reverse; a table is skipped when (mk < min && mk.user != min.user) or
+    max < mk, mk = MemKey(user_key, seq, OP_PUT).  tables: [(min_inner, max_inner)].
+    Returns the indices of the tables Get reads, in order."""
+    import functools
+
+    mins = [_decode_inner(t[0]) for t in tables]
+    order = sorted(range(len(tables)),
+                   key=functools.cmp_to_key(lambda a, b: -1 if _memkey_less(mins[a], mins[b])
+                                            else (1 if _memkey_less(mins[b], mins[a]) else 0)))
+    mk = (user_key, seq, 0)
+    out = []
+    for t in reversed(order):
+        mn, mx = mins[t], _decode_inner(tables[t][1])
+        if (_memkey_less(mk, mn) and user_key != mn[0]) or _memkey_less(mx, mk):
+            continue
+        out.append(t)
+    return out

@@ -1,0 +1,191 @@
+"""GPU: the read side of the filter path and the
+host-pointer pipeline's corner cases.
+
+* The level multi-get (LevelMultiGetFilter: Level::Get's candidate tables,
+  src/revision.cpp:265-310, each checked as SSTableReader::Get does,
+  src/sstable.cpp:238) over 24 cached SSTables, run single-threaded and from 8
+  threads with tables coming and going (and, in a cache too small for the
+  level, evicted under running probes): bin/readpath_test.  Its answers are
+  checked here pair by pair against the oracle (the Python restatement of
+  Level::Get's range test and FilterBlockReader over the same blocks).
+* The filter cache's C-ABI probed from Python threads while other threads put
+  and remove tables.
+* adl_bloom_build_segmented (pipelined groups) with fixed strides whose group
+  starts are not 16-byte aligned, and a build failing mid-pipeline.
+"""
+import os
+import subprocess
+import threading
+import time
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def dev():
+    import torch
+
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    torch.cuda.set_device(0)
+    return torch
+
+
+@pytest.fixture(scope="module")
+def ab():
+    import adlbloom
+
+    adlbloom.lib()
+    return adlbloom
+
+
+def test_level_multiget_threaded_vs_oracle(dev, oracle, tmp_path):
+    exe = os.path.join(ROOT, "adlsm-tree_amd", "bin", "readpath_test")
+    r = subprocess.run([exe, str(tmp_path), "8", "10"], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "phase 1 (level cached) 0 mismatches" in r.stdout and "phase 2 (evicting) 0 mismatches" in r.stdout
+
+    tables = []
+    for line in (tmp_path / "tables.txt").read_text().split("\n"):
+        if line:
+            oid, mn, mx = line.split()
+            tables.append((bytes.fromhex(mn), bytes.fromhex(mx)))
+    assert len(tables) >= 16
+    blocks = [(tmp_path / f"table_{t}.blk").read_bytes() for t in range(len(tables))]
+    readers = []
+    for b in blocks:
+        rd = oracle.FilterBlockReaderOracle()
+        assert rd.init(b) == 0
+        readers.append(rd)
+    queries = [bytes.fromhex(x) for x in (tmp_path / "queries.txt").read_text().split("\n") if x]
+    got = {}
+    for line in (tmp_path / "multiget.txt").read_text().split("\n"):
+        if line:
+            f = line.split()
+            got[int(f[0])] = [(int(p.split(":")[0]), int(p.split(":")[1])) for p in f[1:]]
+    assert len(got) == len(queries)
+    # every table's filter 0 over every query, by the oracle
+    want_bits = []
+    for rd in readers:
+        o1, o2 = rd.filter_range(0)
+        bm = np.frombuffer(rd.block[o1:o2], dtype=np.uint8)
+        want_bits.append(oracle.probe(queries, bm, bits_per_key=rd.bits_per_key))
+    pairs = hits = 0
+    for i, q in enumerate(queries):
+        cand = oracle.level_candidates(tables, q, 2**63 - 1)
+        assert [t for t, _ in got[i]] == cand, i
+        for t, m in got[i]:
+            assert m == want_bits[t][i], (i, t)
+            pairs += 1
+            hits += m
+    assert pairs > len(queries)  # overlapping ranges: several candidates per key
+    assert 0 < hits < pairs
+
+
+def _block(oracle, seed, n, bpk=10):
+    keys = oracle.splitmix_keys16(seed, n)
+    return keys, oracle.filter_block_final([oracle.keys2block(keys, bits_per_key=bpk).tobytes()], bpk)
+
+
+def test_filter_cache_concurrent_put_probe(dev, ab, oracle):
+    """Probes from 4 threads while 2 threads put/remove other tables and
+    re-put the probed ones (no lock is held across a probe's kernel)."""
+    T = 16
+    tabs = [_block(oracle, 1000 + t, 20_000) for t in range(T)]
+    cache = ab.FilterCache(64 << 20, max_tables=64)
+    oids = [b"sst-%02d" % t for t in range(T)]
+    for o, (_, blk) in zip(oids, tabs):
+        cache.put(o, blk)
+    rng = np.random.default_rng(5)
+    n = 20_000
+    table = rng.integers(0, T, n).astype(np.uint32)
+    fresh = oracle.splitmix_keys16(0xF00D, n)
+    q = np.where((rng.integers(0, 2, n) == 1)[:, None],
+                 np.stack([tabs[t][0][i % 20_000] for i, t in enumerate(table)]), fresh)
+    want = np.empty(n, np.uint8)
+    for t in range(T):
+        sel = table == t
+        want[sel] = oracle.probe(q[sel], oracle.keys2block(tabs[t][0]))
+    errors = []
+    stop = threading.Event()
+
+    def prober(k):
+        for r in range(15):
+            got, unc = cache.probe(oids, table, q)
+            if unc or not np.array_equal(got, want):
+                errors.append((k, r, int(unc), int((got != want).sum())))
+
+    def churn(k):
+        i = 0
+        while not stop.is_set():
+            cache.put(b"other-%d-%d" % (k, i % 4), tabs[i % T][1])
+            cache.remove(b"other-%d-%d" % (k, (i + 2) % 4))
+            cache.put(oids[(i * 3 + k) % T], tabs[(i * 3 + k) % T][1])  # replace a probed table
+            i += 1
+
+    th = [threading.Thread(target=prober, args=(k,)) for k in range(4)]
+    ch = [threading.Thread(target=churn, args=(k,)) for k in range(2)]
+    for t in th + ch:
+        t.start()
+    for t in th:
+        t.join()
+    stop.set()
+    for t in ch:
+        t.join()
+    cache.close()
+    assert not errors, errors[:5]
+
+
+@pytest.mark.parametrize("stride", [8, 24])
+def test_pipeline_fixed_stride_unaligned_groups(dev, ab, oracle, stride):
+    """adl_bloom_build_segmented with fixed-stride keys: more than 8 filters (so
+    several pipeline groups), an odd first key, group starts at byte offsets that
+    are not multiples of 16 -- every bitmap equal to the oracle's."""
+    rng = np.random.default_rng(stride)
+    sizes = [3, 1001, 0, 17, 5000, 1, 777, 4096, 33, 12345, 9, 2, 70_000, 11]
+    first = 5  # keys before the first filter: key_begin[0] is odd
+    kb = (first + np.concatenate([[0], np.cumsum(sizes)])).astype(np.uint64)
+    hk = rng.integers(0, 256, (int(kb[-1]) + 3, stride), dtype=np.uint8)
+    nbytes = [ab.bitmap_bytes(s, 10) for s in sizes]
+    boff = np.concatenate([[0], np.cumsum(nbytes)[:-1]]).astype(np.uint64)
+    out = np.zeros(int(sum(nbytes)), dtype=np.uint8)
+    ab.build_segmented_host(hk, kb, out, boff)
+    for f, s in enumerate(sizes):
+        want = oracle.keys2block(hk[int(kb[f]):int(kb[f + 1])])
+        assert np.array_equal(out[int(boff[f]):int(boff[f]) + nbytes[f]], want), f
+
+
+@pytest.mark.parametrize("pinned", [False, True])
+def test_pipeline_fault_mid_pipeline(dev, ab, oracle, monkeypatch, pinned):
+    """A build failing in group 2 (ADL_BLOOM_FAULT_GROUP) returns the error only
+    after every copy into the caller's buffer has finished: the buffer does not
+    change after the call returns.  The next call succeeds."""
+    sizes = [400_000] * 24  # 3 groups of 8 filters
+    kb = np.concatenate([[0], np.cumsum(sizes)]).astype(np.uint64)
+    hk = oracle.splitmix_keys16(99, int(kb[-1]))
+    nbytes = [ab.bitmap_bytes(s, 10) for s in sizes]
+    boff = np.concatenate([[0], np.cumsum(nbytes)[:-1]]).astype(np.uint64)
+    total = int(sum(nbytes))
+    if pinned:
+        keys = dev.from_numpy(hk).pin_memory()
+        out = dev.zeros(total, dtype=dev.uint8).pin_memory()
+        view = lambda: out.numpy().copy()  # noqa: E731
+    else:
+        keys, out = hk, np.zeros(total, dtype=np.uint8)
+        view = lambda: out.copy()  # noqa: E731
+    monkeypatch.setenv("ADL_BLOOM_FAULT_GROUP", "2")
+    with pytest.raises(ab.AdlBloomError):
+        ab.build_segmented_host(keys, kb, out, boff)
+    a = view()
+    time.sleep(0.2)
+    assert np.array_equal(a, view()), "the caller's buffer changed after the error returned"
+    monkeypatch.delenv("ADL_BLOOM_FAULT_GROUP")
+    ab.build_segmented_host(keys, kb, out, boff)
+    full = view()
+    for f in (0, 9, 23):
+        want = oracle.keys2block(hk[int(kb[f]):int(kb[f + 1])])
+        assert np.array_equal(full[int(boff[f]):int(boff[f]) + nbytes[f]], want), f
