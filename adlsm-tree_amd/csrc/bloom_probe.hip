@@ -192,28 +192,39 @@ __global__ __launch_bounds__(256) void synth_probe_kernel(uint4 *__restrict__ ke
 
 constexpr int kZipfR = 249;  // lengths 8 .. 256
 
+// Inverse-CDF table of Zipf(s) on [1, kZipfR] in 53-bit fixed point: r is the
+// first rank with x < thr[r-1], x = a SplitMix64 output >> 11.  Built on the
+// host (zipf_table), so the device and the oracle's restatement
+// (oracle_synth_varlen_lengths) draw identical lengths from the same stream.
+struct ZipfTable {
+  uint64_t thr[kZipfR];
+};
+
 __global__ __launch_bounds__(256) void synth_lengths_kernel(uint32_t *__restrict__ len, uint64_t seed,
-                                                            uint64_t n, double s) {
-  __shared__ double cdf[kZipfR];
-  if (threadIdx.x == 0) {
-    double acc = 0;
-    for (int r = 1; r <= kZipfR; ++r) {
-      acc += pow((double)r, -s);
-      cdf[r - 1] = acc;
-    }
-    for (int r = 0; r < kZipfR; ++r) cdf[r] /= acc;
-  }
-  __syncthreads();
+                                                            uint64_t n, ZipfTable zt) {
   const uint64_t lseed = seed ^ 0xD1B54A32D192ED03ull;
   for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
-    const double u = (double)(splitmix_at(lseed, i + 1) >> 11) * (1.0 / 9007199254740992.0);
-    int lo = 0, hi = kZipfR - 1;  // first r with u < cdf[r]
+    const uint64_t x = splitmix_at(lseed, i + 1) >> 11;
+    int lo = 0, hi = kZipfR - 1;  // first r with x < thr[r]
     while (lo < hi) {
       const int mid = (lo + hi) >> 1;
-      if (u < cdf[mid]) hi = mid; else lo = mid + 1;
+      if (x < zt.thr[mid]) hi = mid; else lo = mid + 1;
     }
     len[i] = 8u + (uint32_t)lo;
   }
+}
+
+// cdf(r) = sum_{i<=r} i^-s / sum_{i<=R} i^-s in double; thr = ceil(cdf * 2^53),
+// so x < thr  <=>  x * 2^-53 < cdf  for every 53-bit integer x
+ZipfTable zipf_table(double s) {
+  ZipfTable z{};
+  double cdf[kZipfR], acc = 0;
+  for (int r = 1; r <= kZipfR; ++r) {
+    acc += pow((double)r, -s);
+    cdf[r - 1] = acc;
+  }
+  for (int r = 0; r < kZipfR; ++r) z.thr[r] = (uint64_t)ceil(cdf[r] / acc * 9007199254740992.0);
+  return z;
 }
 
 __global__ __launch_bounds__(256) void synth_fill_kernel(uint64_t *__restrict__ out, uint64_t seed,
@@ -405,7 +416,7 @@ int adl_synth_varlen_lengths_device(uint32_t *d_lengths, uint64_t seed, uint64_t
   if (n == 0) return ADL_OK;
   if (!d_lengths) return ADL_ERR_INVALID_ARG;
   hipLaunchKernelGGL(synth_lengths_kernel, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream,
-                     d_lengths, seed, n, zipf_s);
+                     d_lengths, seed, n, zipf_table(zipf_s));
   ADL_HIP_TRY(hipGetLastError());
   return ADL_OK;
 }

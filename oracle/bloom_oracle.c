@@ -245,3 +245,42 @@ void oracle_synth_probe_queries(uint64_t seed, uint64_t q0, uint64_t n, uint32_t
     if (member) member[i] = (uint8_t)ins;
   }
 }
+
+/* Variable-length synthetic keys of BASELINE.json configs[2], restating the
+ * device generator (adlsm-tree_amd/csrc/bloom_probe.hip synth_lengths_kernel /
+ * synth_fill_kernel, DESIGN.md "Synthetic inputs"): key i has length
+ * 8 + (r - 1), r ~ Zipf(s) on [1, 249] by inverse CDF -- the first r with
+ * x < ceil(cdf(r) * 2^53), x = output i+1 of the SplitMix64 stream seeded
+ * seed ^ 0xD1B54A32D192ED03, shifted right by 11 -- and byte j of the packed
+ * key buffer is byte j % 8 (little-endian) of output j/8 + 1 of the stream
+ * seeded `seed`.  These are synthetic inputs of the survey's shape (§8d), not
+ * a reference algorithm: the bitmaps built from them are pinned by the
+ * oracle's Keys2Block, which is pinned to the reference. */
+#include <math.h>
+void oracle_synth_varlen_lengths(uint64_t seed, uint64_t n, double s, uint32_t *len) {
+  enum { R = 249 };
+  double cdf[R], acc = 0;
+  uint64_t thr[R];
+  for (int r = 1; r <= R; r++) {
+    acc += pow((double)r, -s);
+    cdf[r - 1] = acc;
+  }
+  for (int r = 0; r < R; r++) thr[r] = (uint64_t)ceil(cdf[r] / acc * 9007199254740992.0);
+  const uint64_t lseed = seed ^ 0xD1B54A32D192ED03ull;
+  for (uint64_t i = 0; i < n; i++) {
+    const uint64_t x = oracle_splitmix_at(lseed, i + 1) >> 11;
+    int lo = 0, hi = R - 1;
+    while (lo < hi) {
+      int mid = (lo + hi) >> 1;
+      if (x < thr[mid]) hi = mid; else lo = mid + 1;
+    }
+    len[i] = 8u + (uint32_t)lo;
+  }
+}
+
+void oracle_synth_varlen_fill(uint64_t seed, uint64_t total_bytes, uint8_t *out) {
+  for (uint64_t w = 0; 8 * w < total_bytes; w++) {
+    const uint64_t z = oracle_splitmix_at(seed, w + 1);
+    for (uint64_t b = 0; b < 8 && 8 * w + b < total_bytes; b++) out[8 * w + b] = (uint8_t)(z >> (8 * b));
+  }
+}

@@ -67,6 +67,10 @@ def lib():
         L.oracle_synth_probe_queries.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
                                                  ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64,
                                                  u8p, u8p, u8p]
+        L.oracle_synth_varlen_lengths.restype = None
+        L.oracle_synth_varlen_lengths.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_double, u8p]
+        L.oracle_synth_varlen_fill.restype = None
+        L.oracle_synth_varlen_fill.argtypes = [ctypes.c_uint64, ctypes.c_uint64, u8p]
         _LIB = L
     return _LIB
 
@@ -110,6 +114,20 @@ def synth_probe_queries(n: int, seed: int = 0xFEED, q0: int = 0, num_tables: int
     lib().oracle_synth_probe_queries(seed, q0, n, num_tables, table_seed0, keys_per_table,
                                      _ptr(keys), _ptr(fid), _ptr(member))
     return keys, fid, member
+
+
+def synth_varlen(n: int, seed: int = 0x5EED, zipf_s: float = 1.1):
+    """configs[2] variable-length keys (restating adl_synth_varlen_*_device):
+    (packed bytes uint8, offsets uint64[n+1])."""
+    lengths = np.empty(max(n, 1), dtype=np.uint32)
+    lib().oracle_synth_varlen_lengths(seed, n, zipf_s, _ptr(lengths))
+    offs = np.zeros(n + 1, dtype=np.uint64)
+    offs[1:] = np.cumsum(lengths[:n], dtype=np.uint64)
+    total = int(offs[-1])
+    data = np.empty(total + 16, dtype=np.uint8)
+    lib().oracle_synth_varlen_fill(seed, total, _ptr(data))
+    data[total:] = 0
+    return data, offs
 
 
 def pack(keys) -> tuple[np.ndarray, np.ndarray]:
