@@ -1,10 +1,13 @@
 """adlbloom.dist -- multi-GPU plumbing for the sharded filter workloads.
 
 The path shards by whole filters (one SSTable's filter never spans GPUs,
-reference src/sstable.cpp:21 builds one filter per table), so there is no
-collective on the data path.  One process per GPU; torch.distributed
-(backend "nccl" = RCCL on ROCm, "gloo" in the CPU tests) is used only to
-combine the throughput counters.  SURVEY.md §8e.
+reference src/sstable.cpp:21 builds one filter per table), so the build has
+no collective on its data path: one process per GPU, and torch.distributed
+(backend "nccl" = RCCL on ROCm, "gloo" in the CPU tests) only combines the
+throughput counters.  The probe does have a real exchange step: a query must
+reach the GPU that holds its table's filter, and its answer must come back to
+the rank that asked (bucket queries by owner, stable, and
+scatter the results back).  route_probe does that with two all-to-alls.
 """
 from __future__ import annotations
 
@@ -55,3 +58,53 @@ def reduce_throughput(keys_local: float, elapsed_local: float, device=None):
     dist.all_reduce(k, op=dist.ReduceOp.SUM)
     dist.all_reduce(e, op=dist.ReduceOp.MAX)
     return k.item(), e.item()
+
+
+def owner_table(num_tables: int, world: int):
+    """(owner rank, index within the owner's shard) of every table id, as numpy arrays."""
+    t = np.arange(num_tables)
+    own = owner_of(t, num_tables, world)
+    first = np.array([table_shard(num_tables, world, r).start for r in range(world)])
+    return own, t - first[own]
+
+
+def route_probe(keys, fid, owner, local_id, probe_fn, group=None, comm_cpu=None):
+    """Multi-get across ranks: this rank's queries (keys (n, 16) uint8, fid (n,)
+    global table ids) are bucketed by the rank owning each table (stable, as
+    partition_queries), sent there (all_to_all), probed against the owner's
+    local filters by probe_fn(keys, local_fid) -> uint8 answers, and the
+    answers sent back (all_to_all) and scattered into the original order.
+    owner / local_id: per-table tensors on keys' device (owner_table).
+    comm_cpu: stage the exchanges through host memory (default: when the
+    backend is gloo, which moves host tensors; RCCL moves device memory).
+    Returns (answers uint8 (n,), queries this rank probed for others)."""
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    dev = keys.device
+    if comm_cpu is None:
+        comm_cpu = dist.get_backend(group) == "gloo" and dev.type != "cpu"
+    fid = fid.long()
+    own = owner[fid]
+    order = torch.sort(own, stable=True).indices
+    counts = torch.bincount(own, minlength=world)
+    xfer = (lambda t: t.cpu()) if comm_cpu else (lambda t: t)
+    back = (lambda t: t.to(dev)) if comm_cpu else (lambda t: t)
+    rcounts = xfer(torch.empty_like(counts))
+    dist.all_to_all_single(rcounts, xfer(counts), group=group)
+    send = counts.tolist()
+    recv = rcounts.tolist()
+    # keys as 2 x int64 per query (16 B), local filter ids as int32
+    k_send = keys[order].contiguous().view(torch.int64).view(-1, 2)
+    f_send = local_id[fid[order]].to(torch.int32)
+    k_recv = torch.empty((sum(recv), 2), dtype=torch.int64, device=xfer(k_send).device)
+    f_recv = torch.empty(sum(recv), dtype=torch.int32, device=k_recv.device)
+    dist.all_to_all_single(k_recv, xfer(k_send), recv, send, group=group)
+    dist.all_to_all_single(f_recv, xfer(f_send), recv, send, group=group)
+    ans = probe_fn(back(k_recv).view(torch.uint8).view(-1, 16), back(f_recv))
+    a_back = torch.empty(sum(send), dtype=torch.uint8, device=k_recv.device)
+    dist.all_to_all_single(a_back, xfer(ans.to(torch.uint8).contiguous()), send, recv, group=group)
+    out = torch.empty(keys.shape[0], dtype=torch.uint8, device=dev)
+    out[order] = back(a_back)
+    return out, int(sum(recv))

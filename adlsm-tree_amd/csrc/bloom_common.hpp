@@ -252,6 +252,39 @@ struct Staging {
 
 inline thread_local Staging t_stage;
 
+// Per-thread small pinned buffer mapped into the device's address space
+// (coherent): a small synchronous probe hands the kernel its keys and table
+// ids where they are and has it write the answers back there, so a lookup is
+// one launch and one stream sync, with no H2D / D2H copy commands.
+struct MappedStage {
+  static constexpr uint64_t kMax = 64 << 10;
+  uint8_t *host = nullptr;
+  uint8_t *dev = nullptr;
+  bool tried = false;
+  ~MappedStage() {
+    if (host) (void)hipHostFree(host);
+  }
+  // nullptr if unavailable or bytes > kMax (the caller then stages and copies)
+  uint8_t *get(uint64_t bytes) {
+    if (bytes > kMax) return nullptr;
+    if (!tried) {
+      tried = true;
+      void *d = nullptr;
+      if (hipHostMalloc((void **)&host, kMax, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+          hipHostGetDevicePointer(&d, host, 0) != hipSuccess) {
+        if (host) (void)hipHostFree(host);
+        host = nullptr;
+        (void)hipGetLastError();
+        return nullptr;
+      }
+      dev = static_cast<uint8_t *>(d);
+    }
+    return host;
+  }
+};
+
+inline thread_local MappedStage t_mapped;
+
 // The stream a synchronous host-pointer entry point runs on: the caller's, or
 // for stream == NULL a non-blocking stream of the calling thread (created on
 // first use).  The legacy null stream would order every thread's calls one

@@ -318,29 +318,39 @@ int adl_bloom_filter_cache_probe(adl_bloom_filter_cache *c, const char *const *o
     const uint64_t o_be = o_fid + adl_host::round_up(n * 4, 256);
     const uint64_t o_out = o_be + adl_host::round_up(be.size() * 8, 256);
     const uint64_t total = o_out + adl_host::round_up(n, 256);
+    // A small batch (a single-key Get) is handed over in the thread's mapped
+    // buffer: the kernel reads it and writes its answers there directly.
     adl_host::Staging &sg = adl_host::t_stage;
-    int rc = sg.reserve(o_out, total);
-    if (rc == ADL_OK) {
-      if (key_bytes) memcpy(sg.host, h_keys, key_bytes);
-      if (off_bytes) memcpy(sg.host + o_offs, h_offsets, off_bytes);
-      memcpy(sg.host + o_fid, h_table, n * 4);
-      memcpy(sg.host + o_be, be.data(), be.size() * 8);
-      if (hipMemcpyAsync(sg.dev, sg.host, o_out, hipMemcpyHostToDevice, st) != hipSuccess) rc = ADL_ERR_DEVICE;
+    uint8_t *hbuf = adl_host::t_mapped.get(total), *dbuf = hbuf ? adl_host::t_mapped.dev : nullptr;
+    int rc = ADL_OK;
+    if (!hbuf) {
+      rc = sg.reserve(total, total);
+      hbuf = sg.host;
+      dbuf = sg.dev;
     }
     if (rc == ADL_OK) {
-      const uint64_t *d_be = reinterpret_cast<const uint64_t *>(sg.dev + o_be);
-      rc = adl_bloom_probe_ranges_device(sg.dev, h_offsets ? reinterpret_cast<uint64_t *>(sg.dev + o_offs) : nullptr,
-                                         n, key_stride, reinterpret_cast<const uint32_t *>(sg.dev + o_fid),
-                                         num_tables, c->arena, d_be, d_be + num_tables, c->bpk, sg.dev + o_out, st);
+      if (key_bytes) memcpy(hbuf, h_keys, key_bytes);
+      if (off_bytes) memcpy(hbuf + o_offs, h_offsets, off_bytes);
+      memcpy(hbuf + o_fid, h_table, n * 4);
+      memcpy(hbuf + o_be, be.data(), be.size() * 8);
+      if (hbuf == sg.host && hipMemcpyAsync(dbuf, hbuf, o_out, hipMemcpyHostToDevice, st) != hipSuccess)
+        rc = ADL_ERR_DEVICE;
     }
-    if (rc == ADL_OK && hipMemcpyAsync(sg.host, sg.dev + o_out, n, hipMemcpyDeviceToHost, st) != hipSuccess)
+    if (rc == ADL_OK) {
+      const uint64_t *d_be = reinterpret_cast<const uint64_t *>(dbuf + o_be);
+      rc = adl_bloom_probe_ranges_device(dbuf, h_offsets ? reinterpret_cast<uint64_t *>(dbuf + o_offs) : nullptr,
+                                         n, key_stride, reinterpret_cast<const uint32_t *>(dbuf + o_fid),
+                                         num_tables, c->arena, d_be, d_be + num_tables, c->bpk, dbuf + o_out, st);
+    }
+    if (rc == ADL_OK && hbuf == sg.host &&
+        hipMemcpyAsync(hbuf + o_out, dbuf + o_out, n, hipMemcpyDeviceToHost, st) != hipSuccess)
       rc = ADL_ERR_DEVICE;
     // the kernel and the copies are done before any pinned range can be reused
     if (hipStreamSynchronize(st) != hipSuccess && rc == ADL_OK) rc = ADL_ERR_DEVICE;
     // 3. unpin (a range retired meanwhile is freed by its last unpin)
     unpin_all();
     if (rc) return rc;
-    memcpy(h_out, sg.host, n);
+    memcpy(h_out, hbuf + o_out, n);
     if (h_uncached) *h_uncached = uncached;
     return ADL_OK;
   } catch (...) {

@@ -75,11 +75,19 @@ RC LevelMultiGetFilter(FilterCache &cache, const vector<TableRange> &tables, con
     return InnerKeyLess(tables[a].min_inner_key, tables[b].min_inner_key);
   });
   std::reverse(visit.begin(), visit.end());
+  // the ranges decoded once (the inner keys outlive this call)
+  vector<Decoded> mn(tables.size()), mx(tables.size());
+  for (size_t t = 0; t < tables.size(); ++t) {
+    mn[t] = Decode(tables[t].min_inner_key);
+    mx[t] = Decode(tables[t].max_inner_key);
+  }
   // candidates of every key, and the probe batch: pair p = (key, table)
   KeyArena batch;
   for (size_t i = 0; i < user_keys.size(); ++i) {
+    const Decoded mk{user_keys[i], seq, 0 /* OP_PUT */};
     for (uint32_t t : visit) {
-      if (!TableCoversKey(tables[t], user_keys[i], seq)) continue;
+      // TableCoversKey, on the decoded ranges
+      if ((Less(mk, mn[t]) && mk.user != mn[t].user) || Less(mx[t], mk)) continue;
       out.table.push_back(t);
       batch.Add(user_keys[i]);  // SSTableReader::Get probes the user key (src/sstable.cpp:238)
     }

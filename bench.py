@@ -8,15 +8,18 @@ pass A (hash + bin) and pass B (LDS tile OR + bitmap write).  Workloads:
 
   single      (default) one 10M x 16 B-key filter per GPU, bpk=10 (BASELINE.json
               configs[1]); weak scaling: rank r builds its own SSTable filter.
-  compaction  32 SSTables x 1M x 16 B keys per GPU in one segmented build
-              (configs[3]: 256 tables over 8 GPUs).
+  compaction  256 SSTables x 1M x 16 B keys, one filter each (configs[3]), tables
+              t -> GPU t // (256/N), each GPU one segmented build of its tables
+              (strong scaling: the 256 tables are fixed).
   varlen      10M variable-length keys (8-256 B, Zipf(1.1) lengths) per GPU (configs[2]).
   probe       100M 16 B queries against 256 device-resident 1M-key filters (configs[4]);
-              filters t -> GPU t // (256/N), each GPU probes the queries of its own
-              filters (strong scaling: the 100M total is fixed).
+              filters t -> GPU t // (256/N); rank r asks queries [r*Q/N, (r+1)*Q/N) of the
+              stream, which travel to their filter's GPU and back (RCCL all-to-all,
+              adlbloom.dist.route_probe) -- strong scaling, the 100M total is fixed.
 
-Multi-GPU: one process per GPU (torch.distributed.run); no collective on the
-data path -- each rank owns whole filters.  RCCL reduces only the key counter
+Multi-GPU: one process per GPU (torch.distributed.run).  The builds have no
+collective on the data path -- each rank owns whole filters; the probe's
+query routing is its one exchange step.  RCCL also reduces the key counter
 (sum) and the elapsed time (max).  Rank 0 prints one JSON line.
 """
 import argparse
@@ -35,6 +38,7 @@ BPK = 10
 ALGO_BYTES_PER_KEY16 = 26  # 16 B key read + (n*bpk+7)/n ~ 10 B bitmap write
 ALGO_BYTES_PER_QUERY = 21  # 16 B query + 4 B filter id + 1 B result
 PROBE_TABLES, PROBE_KEYS_PER_TABLE = 256, 1_000_000
+COMPACTION_TABLES = 256   # BASELINE.json configs[3]
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 
 
@@ -88,26 +92,30 @@ class Workload:
             self.dtype = "u32"
         elif kind == "probe":
             self._init_probe(rank, world, queries)
-        else:  # compaction: 32 tables x 1M keys per GPU; table t lives on GPU t // 32
+        else:  # compaction: 256 tables x 1M keys; table t lives on GPU t // (256/N)
             from adlbloom import dist as D
 
             per = 1_000_000
-            tables = D.table_shard(32 * world, world, rank)
+            tables = D.table_shard(COMPACTION_TABLES, world, rank)
+            self.tables = tables
             T = len(tables)
             self.n = T * per
             self.keys = torch.cat([ab.synth_keys16(per, seed=0x5EED + t) for t in tables])
             kb = np.arange(T + 1, dtype=np.uint64) * per
             self.builder = ab.SegmentedBuilder(kb, BPK)
             self.bytes_per_launch = ALGO_BYTES_PER_KEY16 * self.n
-            self.config = {"workload": "compaction: 32 SSTables x 1M x 16B keys per GPU (256 over 8 GPUs)",
-                           "keys_per_gpu": self.n, "key_bytes": 16, "bits_per_key": BPK, "filters_per_gpu": T}
+            self.config = {"workload": f"compaction: {COMPACTION_TABLES} SSTables x 1M x 16B keys, one filter each, "
+                                       f"{T} per GPU",
+                           "tables_total": COMPACTION_TABLES, "keys_per_gpu": self.n, "key_bytes": 16,
+                           "bits_per_key": BPK, "filters_per_gpu": T}
             self.dtype = "u32"
 
     def _init_probe(self, rank, world, queries):
         """configs[4]: 256 tables x 1M keys (this rank's share built on the device in
-        segmented builds of 32 tables), compacted to exact-length bitmaps; the
-        global query stream is generated on the device and this rank keeps the
-        queries of the filters it owns."""
+        segmented builds of 32 tables), compacted to exact-length bitmaps.  Rank r
+        asks the slice [r*Q/N, (r+1)*Q/N) of the global query stream (generated on
+        the device); at N > 1 each step routes the queries to their filters' ranks
+        and the answers back (adlbloom.dist.route_probe)."""
         import numpy as np
         import torch
 
@@ -117,6 +125,7 @@ class Workload:
         per = PROBE_KEYS_PER_TABLE
         tables = D.table_shard(PROBE_TABLES, world, rank)
         self.tables = tables
+        self.world = world
         pieces, sizes = [], []
         for g0 in range(tables.start, tables.stop, 32):
             grp = range(g0, min(g0 + 32, tables.stop))
@@ -130,32 +139,46 @@ class Workload:
         off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.uint64)
         self.bitmap_off_host = off
         self.bitmap_off = torch.from_numpy(off.view(np.int64)).cuda()
-        # the global query stream in slices; keep this rank's queries (local filter ids)
-        ks, fs, ms = [], [], []
-        step = 25_000_000
-        for q0 in range(0, queries, step):
-            k, f, m = ab.synth_probe_queries(min(step, queries - q0), q0=q0, num_tables=PROBE_TABLES,
-                                             keys_per_table=per)
-            sel = (f >= tables.start) & (f < tables.stop)
-            ks.append(k[sel])
-            fs.append(f[sel] - tables.start)
-            ms.append(m[sel])
-        self.keys, self.fid, self.member = torch.cat(ks), torch.cat(fs), torch.cat(ms)
-        del ks, fs, ms
-        self.n = int(self.keys.shape[0])
+        own, lid = D.owner_table(PROBE_TABLES, world)
+        self.owner = torch.from_numpy(own).cuda()
+        self.local_id = torch.from_numpy(lid).cuda()
+        if queries % world:
+            raise SystemExit(f"--queries {queries} must divide over {world} ranks")
+        self.q0, self.n = rank * (queries // world), queries // world
+        self.keys, self.fid, self.member = ab.synth_probe_queries(self.n, q0=self.q0, num_tables=PROBE_TABLES,
+                                                                  keys_per_table=per)
         self.total_queries = queries
         self.bytes_per_launch = ALGO_BYTES_PER_QUERY * self.n
+        self.kernel_events = []  # (start, stop) of every probe launch
+        self.served = self.n
         self.config = {"workload": f"probe: {queries // 1_000_000}M x 16B queries vs {PROBE_TABLES} device-resident "
                                    f"filters of {per // 1_000_000}M keys (50% inserted keys)",
                        "queries_total": queries, "queries_this_gpu": self.n, "filters_total": PROBE_TABLES,
-                       "filters_per_gpu": len(tables), "keys_per_filter": per, "bits_per_key": BPK}
+                       "filters_per_gpu": len(tables), "keys_per_filter": per, "bits_per_key": BPK,
+                       "routing": "none (one GPU)" if world == 1 else
+                       "RCCL all-to-all of queries to their filter's GPU and of answers back, inside each step"}
         self.dtype = "u32"
+
+    def _probe_local(self, keys, lfid):
+        import torch
+
+        import adlbloom as ab
+
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        out = ab.probe_multi(keys, lfid, self.bitmaps, self.bitmap_off)
+        e1.record()
+        self.kernel_events.append((e0, e1))
+        return out
 
     def step(self):
         if self.kind == "probe":
-            import adlbloom as ab
+            if self.world == 1:
+                return self._probe_local(self.keys, self.fid)
+            from adlbloom import dist as D
 
-            return ab.probe_multi(self.keys, self.fid, self.bitmaps, self.bitmap_off)
+            out, self.served = D.route_probe(self.keys, self.fid, self.owner, self.local_id, self._probe_local)
+            return out
         if self.kind == "varlen":
             return self.builder.build(self.keys, self.offs)
         return self.builder.build(self.keys)
@@ -211,7 +234,7 @@ def cpu_baseline(budget_s, workload="single", w=None):
                 list(ex.map(lambda k: O.keys2block(k, bits_per_key=BPK), tables))
             reps, t = _timed_reps(run, budget_s)
         return {"value": round(T * per * reps / t / 1e6, 3), "unit": "Mkeys/s", "cores": cores, "kind": "port",
-                "sample": f"{reps} x 32 tables x 1M x 16B keys (rank-0 shard), one filter per thread on "
+                "sample": f"{reps} x 32 of the 256 tables x 1M x 16B keys, one filter per thread on "
                           f"{cores} threads, oracle_keys2block (gcc -O2), {t:.1f} s"}
     if workload == "probe":
         cores = _cpu_cores()
@@ -237,51 +260,97 @@ def cpu_baseline(budget_s, workload="single", w=None):
                       f"(C restatement of src/filter_block.cpp:9-33, gcc -O2), {t_total:.1f} s"}
 
 
-def probe_check(w, out):
-    """Probe results: every inserted-key query must hit (full batch, on the
-    device); the false-positive rate over fresh keys; and a 200k-query sample
-    plus two tables' bitmaps compared bit for bit with the oracle."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+def load_pins():
+    """Full-size oracle pins of configs[2]-[4] (tests/golden/full_size.json), or None."""
+    try:
+        with open(os.path.join(ROOT, "tests", "golden", "full_size.json")) as f:
+            return json.load(f)
+    except (OSError, ValueError):
+        return None
+
+
+def gather_all(t, world):
+    """Every rank's equal-length slice, concatenated in rank order (all ranks call)."""
+    if world == 1:
+        return t
+    import torch
+    import torch.distributed as dist
+
+    if dist.get_backend() == "gloo":  # host tensors (the 2-rank test on one GPU)
+        parts = [torch.empty_like(t.cpu()) for _ in range(world)]
+        dist.all_gather(parts, t.contiguous().cpu())
+        return torch.cat(parts).to(t.device)
+    out = torch.empty(world * t.numel(), dtype=t.dtype, device=t.device)
+    dist.all_gather_into_tensor(out, t.contiguous())
+    return out
+
+
+def probe_check(w, out, rank, world):
+    """Probe results (all ranks call; rank 0 returns the record): all 100M answers,
+    gathered in global query order, against the oracle's SHA-256
+    (tests/golden/full_size.json); every inserted key found; the false-positive
+    rate on fresh keys; and the bitmap reads per query with the reference's early
+    exit, counted on a sample of rank 0's queries to its own filters."""
     import numpy as np
 
+    allout = gather_all(out, world)
+    allmem = gather_all(w.member, world)
+    if rank != 0:
+        return None
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
 
-    mem = w.member.bool()
-    hits_ins = int(out[mem].sum().item())
+    mem = allmem.bool()
+    hits_ins = int(allout[mem].sum().item())
     n_ins = int(mem.sum().item())
-    fp = int(out[~mem].sum().item())
-    n_fresh = w.n - n_ins
-    ns = min(w.n, 200_000)
+    fp = int(allout[~mem].sum().item())
+    n_fresh = int(allout.numel()) - n_ins
+    rec = {"hit_rate_inserted": round(hits_ins / max(n_ins, 1), 6), "false_negatives": n_ins - hits_ins,
+           "fpr_fresh": round(fp / max(n_fresh, 1), 6), "queries_inserted": n_ins, "queries_fresh": n_fresh}
+    pins = load_pins()
+    if pins and pins["probe"]["queries"] == w.total_queries:
+        sha = hashlib.sha256(allout.cpu().numpy().tobytes()).hexdigest()
+        rec["oracle"] = ("all %dM answers bit-identical to the oracle (sha256)" % (w.total_queries // 1_000_000)
+                         if sha == pins["probe"]["results_sha256"] else f"MISMATCH sha256 {sha}")
+    # reads per query on rank 0's own filters
+    fid_all = w.fid.cpu().numpy().astype(np.int64)
+    sel = np.nonzero((fid_all >= w.tables.start) & (fid_all < w.tables.stop))[0][:200_000]
     bms = w.bitmaps.cpu().numpy()
-    off = w.bitmap_off_host
-    want = O.probe_multi(w.keys[:ns].cpu().numpy(), w.fid[:ns].cpu().numpy().view(np.uint32), bms, off,
-                         bits_per_key=BPK)
-    sample_ok = bool(np.array_equal(out[:ns].cpu().numpy(), want))
-    tab_ok = True
-    for li in (0, len(w.tables) - 1):
-        t = w.tables[li]
-        ref = O.keys2block(O.splitmix_keys16(0x5EED + t, PROBE_KEYS_PER_TABLE), bits_per_key=BPK)
-        tab_ok &= bool(np.array_equal(bms[int(off[li]):int(off[li + 1])], ref))
-    # bitmap byte reads per query with the reference's early exit (src/filter_block.cpp:54-59),
-    # counted on the sample: the probe's real work unit (k random reads at most)
-    h = O.murmur3_batch(w.keys[:ns].cpu().numpy())
-    fid = w.fid[:ns].cpu().numpy().astype(np.int64)
-    base = np.asarray(off, dtype=np.int64)[fid]
-    m = (np.asarray(off, dtype=np.int64)[fid + 1] - base) * 8
-    alive = np.ones(ns, dtype=bool)
-    reads = np.zeros(ns, dtype=np.int64)
+    off = np.asarray(w.bitmap_off_host, dtype=np.int64)
+    h = O.murmur3_batch(w.keys.cpu().numpy()[sel])
+    lf = fid_all[sel] - w.tables.start
+    base = off[lf]
+    m = (off[lf + 1] - base) * 8
+    alive = np.ones(sel.size, dtype=bool)
+    reads = np.zeros(sel.size, dtype=np.int64)
     for j in range(O.num_probes(BPK)):
         pos = ((h[:, 0].astype(np.uint64) + np.uint64(j) * h[:, 1].astype(np.uint64)) % np.uint64(1 << 32)
                ).astype(np.int64) % m
         bit = (bms[base + (pos >> 3)] >> (pos & 7)) & 1
         reads += alive
         alive &= bit.astype(bool)
-    return {"hit_rate_inserted": round(hits_ins / max(n_ins, 1), 6), "false_negatives": n_ins - hits_ins,
-            "bitmap_reads_per_query": round(float(reads.mean()), 4),
-            "fpr_fresh": round(fp / max(n_fresh, 1), 6), "queries_inserted": n_ins, "queries_fresh": n_fresh,
-            "oracle_sample": f"{ns} queries {'bit-identical' if sample_ok else 'MISMATCH'} vs oracle_probe_multi",
-            "oracle_bitmaps": "tables %d,%d %s" % (w.tables[0], w.tables[-1],
-                                                   "bit-identical" if tab_ok else "MISMATCH")}
+    rec["bitmap_reads_per_query"] = round(float(reads.mean()), 4)
+    return rec
+
+
+def build_parity(w, rank):
+    """Rank 0's bitmaps against the oracle pins (varlen, compaction)."""
+    pins = load_pins()
+    if rank != 0 or not pins:
+        return None
+    if w.kind == "varlen":
+        p = pins["varlen"]
+        if w.n != p["n"]:
+            return None
+        sha = hashlib.sha256(w.builder.bitmap[:w.builder.nbytes].cpu().numpy().tobytes()).hexdigest()
+        return "bit-identical to the oracle (sha256)" if sha == p["bitmap_sha256"] else f"MISMATCH sha256 {sha}"
+    if w.kind == "compaction":
+        want = pins["compaction"]["bitmap_sha256"]
+        bad = [t for i, t in enumerate(w.tables)
+               if hashlib.sha256(w.builder.bitmap(i).cpu().numpy().tobytes()).hexdigest() != want[t]]
+        return (f"all {len(w.tables)} bitmaps of this GPU bit-identical to the oracle (sha256)" if not bad
+                else f"MISMATCH tables {bad[:8]}")
+    return None
 
 
 def hbm_stream_read_gbs(nbytes=4 << 30, reps=5):
@@ -471,21 +540,20 @@ def main():
         w.step()
     barrier()
     ab.profile_enable(max(args.steps, 1) * 64)  # launch pairs: a segmented build runs one per 8 filters
-    # probe: one kernel per step on torch's current stream, bracketed by events there
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(args.steps)] if probe else []
+    # probe: one kernel per step on torch's current stream, bracketed by events
+    # there (Workload._probe_local); at N > 1 the routing runs around it
+    if probe:
+        w.kernel_events = []
     t0 = time.perf_counter()
     for i in range(args.steps):
-        if probe:
-            ev[i][0].record()
         out = w.step()
-        if probe:
-            ev[i][1].record()
     barrier()
     elapsed = time.perf_counter() - t0
     pairs = ab.profile_each(max(args.steps, 1) * 64)
     ms_a, ms_b, nb = ab.profile_collect()
-    probe_ms = sum(a.elapsed_time(b) for a, b in ev) / max(args.steps, 1) if probe else 0.0
+    probe_ms = sum(a.elapsed_time(b) for a, b in w.kernel_events) / max(args.steps, 1) if probe else 0.0
+    if probe:  # the kernel's own work: the queries this rank probed (its filters' share of all ranks')
+        w.bytes_per_launch = ALGO_BYTES_PER_QUERY * w.served
 
     # RCCL: the only collective -- sum of keys built, max of elapsed time
     from adlbloom import dist as D
@@ -495,8 +563,10 @@ def main():
     parity = None
     if rank == 0 and args.workload == "single":
         parity = parity_check(out, w.n)
-    elif rank == 0 and probe:
-        parity = probe_check(w, out)
+    elif probe:
+        parity = probe_check(w, out, rank, world)
+    else:
+        parity = build_parity(w, rank)
 
     if rank == 0:
         if probe:
@@ -538,7 +608,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(elapsed_max / max(args.steps, 1) * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "strong" if probe else "weak",
+            "scaling": "strong" if args.workload in ("probe", "compaction") else "weak",
             "vs_baseline": None,
             "dtype": w.dtype,
             "data": "synthetic (SplitMix64 keys generated on device, SURVEY.md §8d)",
@@ -566,7 +636,7 @@ def main():
         if probe and parity and timed:
             # the probe's real ceiling: random bitmap byte reads (k per query at most)
             rr = hbm_random_read_gps(w.bitmaps)
-            gps = parity["bitmap_reads_per_query"] * w.n / (kern_ms * 1e-3) / 1e9
+            gps = parity["bitmap_reads_per_query"] * w.served / (kern_ms * 1e-3) / 1e9
             out_json["roofline"]["random_reads"] = {
                 "reads_per_query": parity["bitmap_reads_per_query"],
                 "achieved_greads_per_s": round(gps, 2),

@@ -98,3 +98,66 @@ def test_two_ranks_gloo_sharded_build_and_counter_reduce():
     for _, tables, built, _, _ in out:
         for t in tables:
             assert built[t] == O.keys2block(O.splitmix_keys16(0x5EED + t, 2000)).tobytes()
+
+
+def _probe_worker(rank, world, port, q):
+    """route_probe over gloo: rank r originates queries [r*Q/world, (r+1)*Q/world)
+    of the configs[4] stream (scaled down) and gets every answer back in order."""
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "adlsm-tree_amd"))
+    sys.path.insert(0, os.path.join(root, "oracle"))
+    import torch
+    import torch.distributed as dist
+
+    from adlbloom import dist as D
+    import oracle as O
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        T, per, Q = 16, 3000, 20000
+        tables = D.table_shard(T, world, rank)
+        bms = [O.keys2block(O.splitmix_keys16(0x5EED + t, per)) for t in tables]
+        arena = np.concatenate(bms)
+        off = np.concatenate([[0], np.cumsum([b.size for b in bms])]).astype(np.uint64)
+        own, lid = D.owner_table(T, world)
+        q0, n = rank * Q // world, Q // world
+        k, f, m = O.synth_probe_queries(n, q0=q0, num_tables=T, keys_per_table=per)
+        probed = []
+
+        def probe_fn(keys, lfid):
+            probed.append(int(keys.shape[0]))
+            return torch.from_numpy(O.probe_multi(keys.numpy(), lfid.numpy().astype(np.uint32), arena, off))
+
+        out, served = D.route_probe(torch.from_numpy(k), torch.from_numpy(f.astype(np.int64)),
+                                    torch.from_numpy(own), torch.from_numpy(lid), probe_fn)
+        q.put((rank, out.numpy().tobytes(), served, q0, n))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_ranks_gloo_probe_routing_matches_single_process():
+    import torch.multiprocessing as mp
+
+    import oracle as O
+
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_probe_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = sorted(q.get(timeout=180) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    T, per, Q = 16, 3000, 20000
+    bms = [O.keys2block(O.splitmix_keys16(0x5EED + t, per)) for t in range(T)]
+    off = np.concatenate([[0], np.cumsum([b.size for b in bms])]).astype(np.uint64)
+    k, f, m = O.synth_probe_queries(Q, num_tables=T, keys_per_table=per)
+    want = O.probe_multi(k, f, np.concatenate(bms), off)
+    got = np.concatenate([np.frombuffer(o[1], dtype=np.uint8) for o in out])
+    assert np.array_equal(got, want)
+    assert sum(o[2] for o in out) == Q  # every query probed exactly once, by its table's owner
+    assert got[m.astype(bool)].all()

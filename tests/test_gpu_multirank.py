@@ -1,0 +1,92 @@
+"""GPU, world size 2: bench.py's real sharded workloads with GPU builds, two
+processes on cuda:0 over gloo (RCCL refuses two ranks on one GPU; the 8-GPU
+RCCL run is the driver's).  SURVEY.md §8e:
+
+* compaction -- the 256 tables of configs[3] split 128 / 128 by
+  adlbloom.dist.table_shard, each rank one segmented build of its share;
+  every table of both ranks against the oracle's SHA-256
+  (tests/golden/full_size.json);
+* probe -- configs[4]'s 100M queries, rank r asking [r*50M, (r+1)*50M),
+  routed to the rank owning each query's filter and back
+  (adlbloom.dist.route_probe, two all-to-alls); the 100M answers, gathered in
+  query order, against the oracle's SHA-256.
+"""
+import json
+import os
+import socket
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, q):
+    import hashlib
+    import sys
+
+    sys.path.insert(0, ROOT)
+    import torch
+    import torch.distributed as dist
+
+    import bench
+
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        res = {}
+        w = bench.Workload("compaction", rank, 0, world, 0)
+        w.step()
+        torch.cuda.synchronize()
+        res["tables"] = list(w.tables)
+        res["sha"] = [hashlib.sha256(w.builder.bitmap(i).cpu().numpy().tobytes()).hexdigest()
+                      for i in range(len(w.tables))]
+        del w
+        torch.cuda.empty_cache()
+        p = bench.Workload("probe", rank, 0, world, 100_000_000)
+        out = p.step()
+        out = p.step()  # twice: routing state does not leak between steps
+        torch.cuda.synchronize()
+        res["served"] = p.served
+        allout = bench.gather_all(out, world)
+        if rank == 0:
+            res["probe_sha"] = hashlib.sha256(allout.cpu().numpy().tobytes()).hexdigest()
+        q.put((rank, res))
+    except Exception as e:  # report, do not hang the other rank's test
+        q.put((rank, {"error": repr(e)}))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_ranks_one_gpu_compaction_and_probe_routing():
+    import torch.multiprocessing as mp
+
+    with open(os.path.join(ROOT, "tests", "golden", "full_size.json")) as f:
+        pins = json.load(f)
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=280) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    for r in range(world):
+        assert "error" not in out[r], out[r]
+    assert [p.exitcode for p in procs] == [0, 0]
+    want = pins["compaction"]["bitmap_sha256"]
+    assert out[0]["tables"] + out[1]["tables"] == list(range(256))
+    for r in range(world):
+        for t, sha in zip(out[r]["tables"], out[r]["sha"]):
+            assert sha == want[t], (r, t)
+    assert out[0]["served"] + out[1]["served"] == 100_000_000
+    assert out[0]["probe_sha"] == pins["probe"]["results_sha256"]
