@@ -44,7 +44,7 @@ EXPORTS = (
     "adl_bloom_murmur3_device", "adl_bloom_murmur3", "adl_synth_keys16_device",
     "adl_synth_varlen_lengths_device", "adl_synth_varlen_fill_device",
     "adl_bloom_profile_enable", "adl_bloom_profile_collect", "adl_synth_probe_queries_device",
-    "adl_bloom_profile_each",
+    "adl_bloom_profile_each", "adl_bloom_probe_batch_workspace_bytes", "adl_bloom_probe_batch_device",
 )
 
 _LIB = None
@@ -91,6 +91,8 @@ def lib() -> ctypes.CDLL:
         "adl_bloom_filter_cache_probe": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_char_p), vp, u32, u32, vp, vp,
                                                          u64, u32, vp, vp, ctypes.POINTER(u64), vp]),
         "adl_bloom_probe_device": (ctypes.c_int, [vp, vp, u64, u32, i32, vp, u64, vp, vp]),
+        "adl_bloom_probe_batch_workspace_bytes": (u64, [u64, u32, i32, u32]),
+        "adl_bloom_probe_batch_device": (ctypes.c_int, [vp, vp, u64, u32, vp, u32, vp, vp, vp, i32, vp, vp, u64, vp]),
         "adl_bloom_probe_multi_device": (ctypes.c_int, [vp, vp, u64, u32, vp, u32, vp, vp, i32, vp, vp]),
         "adl_bloom_probe": (ctypes.c_int, [vp, vp, u64, u32, i32, vp, u64, vp, vp]),
         "adl_bloom_filter_set_create": (ctypes.c_int, [vp, vp, u32, i32, ctypes.POINTER(vp)]),
@@ -323,6 +325,23 @@ def probe_multi(keys, filter_id, bitmaps, bitmap_off, offsets=None, bits_per_key
     _check(lib().adl_bloom_probe_multi_device(pk, po, n, stride, _dptr(filter_id), bitmap_off.numel() - 1,
                                               _dptr(bitmaps), _dptr(bitmap_off), bits_per_key,
                                               _dptr(out), _stream(stream)), "adl_bloom_probe_multi_device")
+    return out[:n]
+
+
+def probe_batch(keys, filter_id, bitmaps, bitmap_off, offsets=None, bits_per_key: int = 10, stream=None,
+                bitmap_end=None):
+    """Large-batch multi-filter probe (adl_bloom_probe_batch_device): the answers of
+    probe_multi, through the tile-binned pipeline when the batch is large.  The
+    workspace comes from torch's caching allocator."""
+    pk, po, n, stride = _keyset(keys, offsets)
+    F = bitmap_off.numel() - (0 if bitmap_end is not None else 1)
+    L = lib()
+    wsb = L.adl_bloom_probe_batch_workspace_bytes(n, F, bits_per_key, stride)
+    ws = empty_device(wsb, keys.device)
+    out = _torch().empty(max(n, 1), dtype=_torch().uint8, device=keys.device)
+    _check(L.adl_bloom_probe_batch_device(pk, po, n, stride, _dptr(filter_id), F, _dptr(bitmaps), _dptr(bitmap_off),
+                                          _dptr(bitmap_end), bits_per_key, _dptr(out), _dptr(ws), wsb,
+                                          _stream(stream)), "adl_bloom_probe_batch_device")
     return out[:n]
 
 

@@ -88,9 +88,10 @@ __global__ __launch_bounds__(kBlockP) void bloom_probe_multi_kernel(
   const bool lds_tab = nf <= kLdsFilters;
   if (lds_tab) {
     for (uint32_t f = threadIdx.x; f < nf; f += kBlockP) {
-      // an empty range (m = 0: a filter the table does not have) answers 0
-      // below and needs no divisor; fastmod_for(0) would divide by zero
-      const uint32_t m = (uint32_t)(((bend ? bend[f] : boff[f + 1]) - boff[f]) * 8);
+      // an empty range (m = 0: a filter the table does not have) and a filter
+      // of 2^31 bits or more answer 0 below and need no divisor
+      const uint64_t bytes = (bend ? bend[f] : boff[f + 1]) - boff[f];
+      const uint32_t m = bytes <= 0x0fffffffull ? (uint32_t)(bytes * 8) : 0u;
       const FastMod fm = m ? fastmod_for(m) : FastMod{};
       lmod[f] = ModLds{fm.magic, fm.shift};
     }
@@ -102,7 +103,9 @@ __global__ __launch_bounds__(kBlockP) void bloom_probe_multi_kernel(
     uint8_t hit = 0;
     if (f < nf) {
       const uint64_t b0 = boff[f], b1 = bend ? bend[f] : boff[f + 1];
-      const uint32_t m = (uint32_t)((b1 - b0) * 8);
+      // 0 for an empty filter or one of 2^31 bits or more (outside the
+      // reference's int m, src/filter_block.cpp:50)
+      const uint32_t m = b1 - b0 <= 0x0fffffffull ? (uint32_t)((b1 - b0) * 8) : 0u;
       if (m != 0) {
         FastMod mod;
         if (lds_tab) {

@@ -187,6 +187,23 @@ int adl_bloom_probe_ranges_device(const uint8_t *d_keys, const uint64_t *d_offse
                                   const uint64_t *d_begin, const uint64_t *d_end,
                                   int32_t bits_per_key, uint8_t *d_out, void *stream);
 
+/* Large-batch probe with a workspace: the answers of adl_bloom_probe_multi_device
+ * (d_bitmap_end == NULL) or adl_bloom_probe_ranges_device (filter f =
+ * d_bitmaps[d_bitmap_off[f] .. d_bitmap_end[f])).  For big batches of 16-byte
+ * keys over up to 4096 filters (n >= 2^20) it runs the tile-binned pipeline
+ * (queries grouped by filter, positions sorted by 2^20-bit tile, bits tested
+ * in LDS: streaming traffic instead of random bitmap reads);
+ * otherwise the direct kernel.  A filter of 0 bytes or of 2^31 bits or more
+ * answers 0.  Replaces BloomFilter::IsKeyExists (src/filter_block.cpp:49-62)
+ * over a multi-get batch.  d_workspace: 256-byte aligned,
+ * adl_bloom_probe_batch_workspace_bytes(n, num_filters, bpk, key_stride) bytes. */
+uint64_t adl_bloom_probe_batch_workspace_bytes(uint64_t n, uint32_t num_filters, int32_t bits_per_key,
+                                               uint32_t key_stride);
+int adl_bloom_probe_batch_device(const uint8_t *d_keys, const uint64_t *d_offsets, uint64_t n, uint32_t key_stride,
+                                 const uint32_t *d_filter_id, uint32_t num_filters, const uint8_t *d_bitmaps,
+                                 const uint64_t *d_bitmap_off, const uint64_t *d_bitmap_end, int32_t bits_per_key,
+                                 uint8_t *d_out, void *d_workspace, uint64_t workspace_bytes, void *stream);
+
 /* Host-pointer convenience for adl_bloom_probe_device.  Synchronous. */
 int adl_bloom_probe(const uint8_t *h_keys, const uint64_t *h_offsets, uint64_t n,
                     uint32_t key_stride, int32_t bits_per_key, const uint8_t *h_bitmap,

@@ -156,7 +156,7 @@ int oracle_probe(const uint8_t *keys, const uint64_t *offsets, uint64_t n, uint6
 
 /* Multi-filter probe: query i goes to filter filter_id[i], whose bitmap is
  * bitmaps[bitmap_off[f] .. bitmap_off[f+1]).  Same semantics as
- * oracle_probe per query; an out-of-range filter id answers 0, as
+ * oracle_probe per query (an empty filter answers 0); an out-of-range filter id answers 0, as
  * FilterBlockReader::IsKeyExists does for filter_block_num >= filters_nums_
  * (src/filter_block.cpp:174). */
 int oracle_probe_multi(const uint8_t *keys, const uint64_t *offsets, uint64_t n, uint64_t stride,
@@ -167,7 +167,10 @@ int oracle_probe_multi(const uint8_t *keys, const uint64_t *offsets, uint64_t n,
     uint32_t f = filter_id[i];
     if (f >= num_filters) { out[i] = 0; continue; }
     uint64_t bytes = bitmap_off[f + 1] - bitmap_off[f];
-    if (bytes == 0 || bytes * 8 > 0x7fffffffull) return -1;
+    /* an empty filter: the reference divides by zero (h % 0); the GPU path
+     * answers 0, and so does this */
+    if (bytes == 0) { out[i] = 0; continue; }
+    if (bytes * 8 > 0x7fffffffull) return -1;
     uint32_t m = (uint32_t)(bytes * 8);
     const uint8_t *bm = bitmaps + bitmap_off[f];
     uint64_t len;

@@ -1,0 +1,118 @@
+"""GPU: the large-batch probe (adl_bloom_probe_batch_device) against the oracle.
+
+For 16-byte keys and n >= 2^20 it runs the tile-binned pipeline
+(csrc/probe_binned.hip: queries grouped by filter, positions sorted by tile,
+bits tested in LDS); every answer must equal BloomFilter::IsKeyExists
+(src/filter_block.cpp:49-62) per query -- oracle_probe_multi -- and the direct
+kernel's.  Cases: the configs[4] shape scaled down, filters of every size
+class (1 key, under one tile, many tiles, 0 bytes) packed at unaligned
+offsets, ids past the last filter, several bits_per_key, ranges with gaps,
+and batch sizes around the binned threshold.  The full 100M-query configs[4]
+is in test_gpu_full_size.py.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev():
+    import torch
+
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    torch.cuda.set_device(0)
+    return torch
+
+
+@pytest.fixture(scope="module")
+def ab():
+    import adlbloom
+
+    adlbloom.lib()
+    return adlbloom
+
+
+def _arena(oracle, sizes, bpk=10, seed0=0x5EED):
+    bms = [oracle.keys2block(oracle.splitmix_keys16(seed0 + t, n), bits_per_key=bpk) if n else
+           np.zeros(0, np.uint8) for t, n in enumerate(sizes)]
+    off = np.concatenate([[0], np.cumsum([b.size for b in bms])]).astype(np.uint64)
+    arena = np.concatenate(bms + [np.zeros(16, np.uint8)])
+    return arena, off
+
+
+def _check(dev, ab, oracle, arena, off, keys, fid, bpk=10):
+    d_arena = dev.from_numpy(arena).cuda()
+    d_off = dev.from_numpy(off.view(np.int64)).cuda()
+    d_keys = dev.from_numpy(keys).cuda()
+    d_fid = dev.from_numpy(fid.view(np.int32)).cuda()
+    got = ab.probe_batch(d_keys, d_fid, d_arena, d_off, bits_per_key=bpk).cpu().numpy()
+    direct = ab.probe_multi(d_keys, d_fid, d_arena, d_off, bits_per_key=bpk).cpu().numpy()
+    want = oracle.probe_multi(keys, fid, arena, off, bits_per_key=bpk)
+    assert np.array_equal(direct, want)
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, f"{bad.size} answers differ, first at {bad[:5]}"
+    return got
+
+
+def test_probe_batch_config4_shape(dev, ab, oracle):
+    T, per, n = 64, 100_000, 3_000_000
+    arena, off = _arena(oracle, [per] * T)
+    k, f, m = oracle.synth_probe_queries(n, num_tables=T, keys_per_table=per)
+    got = _check(dev, ab, oracle, arena, off, k, f)
+    assert got[m.astype(bool)].all()
+
+
+@pytest.mark.parametrize("bpk", [1, 3, 10, 20])
+def test_probe_batch_filter_sizes_and_ids(dev, ab, oracle, bpk):
+    # 1 key, 13 keys, under one tile, a few tiles, many tiles, empty; packed at odd offsets
+    sizes = [1, 13, 50_000, 0, 300_000, 1_500_000, 7, 0, 120_000]
+    arena, off = _arena(oracle, sizes, bpk=bpk, seed0=77)
+    rng = np.random.default_rng(bpk)
+    n = (1 << 20) + 12345
+    F = len(sizes)
+    fid = rng.integers(0, F + 2, n).astype(np.uint32)  # ids F, F+1: past the last filter -> 0
+    keys = oracle.splitmix_keys16(5, n)
+    # half the queries are keys of their filter
+    ins = rng.integers(0, 2, n).astype(bool)
+    for t, sz in enumerate(sizes):
+        sel = np.nonzero(ins & (fid == t))[0]
+        if sz and sel.size:
+            keys[sel] = oracle.splitmix_keys16(77 + t, sz)[rng.integers(0, sz, sel.size)]
+    got = _check(dev, ab, oracle, arena, off, keys, fid, bpk=bpk)
+    assert not got[fid >= F].any()
+    assert not got[np.isin(fid, [3, 7])].any()  # empty filters answer 0
+
+
+@pytest.mark.parametrize("n", [(1 << 20) - 1, 1 << 20, (1 << 20) + 1])
+def test_probe_batch_threshold(dev, ab, oracle, n):
+    T = 16
+    arena, off = _arena(oracle, [40_000] * T)
+    k, f, _ = oracle.synth_probe_queries(n, num_tables=T, keys_per_table=40_000)
+    _check(dev, ab, oracle, arena, off, k, f)
+
+
+def test_probe_batch_ranges_with_gaps(dev, ab, oracle):
+    """Filters anywhere in an arena (begin/end per filter, gaps and any order),
+    as the filter cache lays them out."""
+    sizes = [30_000, 200_000, 5, 70_000]
+    bms = [oracle.keys2block(oracle.splitmix_keys16(900 + t, s)) for t, s in enumerate(sizes)]
+    arena = np.zeros(sum(b.size for b in bms) + 4096, np.uint8)
+    begin, end, o = [], [], 1000
+    for b in reversed(bms):  # stored in reverse order, with gaps of odd sizes
+        arena[o:o + b.size] = b
+        begin.insert(0, o)
+        end.insert(0, o + b.size)
+        o += b.size + 333
+    n = (1 << 20) + 99
+    rng = np.random.default_rng(3)
+    fid = rng.integers(0, 4, n).astype(np.uint32)
+    keys = oracle.splitmix_keys16(11, n)
+    want = np.empty(n, np.uint8)
+    for t in range(4):
+        sel = fid == t
+        want[sel] = oracle.probe(keys[sel], bms[t])
+    d = lambda a: dev.from_numpy(a).cuda()  # noqa: E731
+    got = ab.probe_batch(d(keys), d(fid.view(np.int32)), d(arena), d(np.array(begin, np.int64)),
+                         bitmap_end=d(np.array(end, np.int64))).cpu().numpy()
+    assert np.array_equal(got, want)
