@@ -15,12 +15,14 @@
 //
 //   K0  per filter: m, the fastmod magic, its 2^20-bit tiles (one launch of
 //       one workgroup, from the device offsets)
-//   K1  per block of 16K queries: LDS histogram of the filter ids
+//   K1  per block of 8K queries: LDS histogram of the filter ids
 //   K2  per filter: its queries' start in filter order, its chunks of C
-//       queries and its (tile, chunk) table; the per-block histograms become
-//       each block's starting slot in every filter's run
-//   K3  per block: each query's slot in filter order (dest), and its two
-//       murmur hashes stored there: the batch grouped by filter, 8 B a query
+//       queries and its (tile, chunk) table; and each block's starting slot
+//       in every filter's run
+//   K3  per block: both murmur hashes of every query, counting-sorted by
+//       filter in LDS and written out run by run (whole lines) to the
+//       query's slot in filter order: the batch grouped by filter, 8 B a
+//       query; and the query's place in the block's sorted order (2 B)
 //   P1  per chunk (C queries of one filter): the k positions of every query,
 //       counting-sorted in LDS by tile, written as u32 entries
 //       qlocal << 20 | offset-in-tile; answers initialised to 1
@@ -28,12 +30,14 @@
 //       every chunk's run of entries for the tile gathered and tested there;
 //       a clear bit stores 0 into its query's answer (only zeros are stored,
 //       so the racing stores of different tiles agree)
-//   K6  per query: out[i] = answer[dest[i]]
+//   K6  per block: the block's answers gathered run by run into LDS, then
+//       out[i] = answer at the query's place (coalesced throughout)
 // Algorithmic traffic per query: 16 B key + 4 B id + 1 B answer; the
 // pipeline moves ~130 B of streaming traffic per query instead of ~4.4
 // random 64-B requests.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -45,7 +49,7 @@ using namespace adl_dev;
 namespace {
 
 constexpr int kBlk = 1024;
-constexpr uint32_t kQB = 16384;                 // queries per bucketing block (K1, K3)
+constexpr uint32_t kQB = 8192;                  // queries per bucketing block (K1, K3, K6)
 constexpr uint32_t kQPT = kQB / kBlk;
 constexpr uint32_t kTL = 20;                    // tile = 2^20 bits = 128 KiB of LDS
 constexpr uint32_t kTileBytes = 1u << (kTL - 3);
@@ -54,6 +58,7 @@ constexpr uint32_t kMaxC = 4096;                // entry = qlocal (12 bits) << 2
 constexpr uint32_t kCPT = kMaxC / kBlk;         // queries per thread in P1
 constexpr uint32_t kMaxBucketFilters = 4096;    // LDS histograms of K1 / K3
 constexpr uint32_t kSentinel = 0xFFFFFFFFu;
+constexpr uint16_t kNoSlot = 0xFFFF;            // a query that is answered 0 without probing
 constexpr uint32_t kLdsWords = 40960;           // 160 KiB
 constexpr uint64_t kMinBinned = 1ull << 20;     // below this the direct kernel wins
 
@@ -75,7 +80,7 @@ struct Plan {
   uint32_t F = 0, k = 0, C = 0, nb = 0;
   uint64_t maxch = 0;
   // workspace byte offsets
-  uint64_t o_desc, o_scal, o_hist, o_cf, o_dest, o_hs, o_ent, o_tab, o_res, total;
+  uint64_t o_desc, o_scal, o_cnt, o_start, o_cf, o_dest, o_hs, o_ent, o_tab, o_res, total;
 };
 
 Plan make_plan(uint64_t n, uint32_t F, int32_t bpk) {
@@ -96,9 +101,10 @@ Plan make_plan(uint64_t n, uint32_t F, int32_t bpk) {
   };
   p.o_desc = take((uint64_t)(F + 1) * sizeof(PFilter));
   p.o_scal = take(256);
-  p.o_hist = take((uint64_t)(F + 1) * p.nb * 4);
+  p.o_cnt = take((uint64_t)(F + 1) * p.nb * 4);
+  p.o_start = take((uint64_t)(F + 1) * p.nb * 4);
   p.o_cf = take(p.maxch * 4);
-  p.o_dest = take(n * 4);
+  p.o_dest = take(n * 2);
   p.o_hs = take(n * 8);
   p.o_ent = take(p.maxch * p.k * p.C * 4);
   p.o_tab = take(p.maxch * (kMaxTiles + 1) * 4);
@@ -150,28 +156,33 @@ __global__ __launch_bounds__(kBlk) void pb_hist_kernel(const uint32_t *__restric
                                                        uint32_t *__restrict__ hist) {
   extern __shared__ uint32_t lds[];
   uint32_t *lh = lds, *ltiles = lds + F + 1;
+  const uint64_t i0 = (uint64_t)blockIdx.x * kQB + threadIdx.x;
+  uint32_t fq[kQPT];  // in flight while the counters are cleared
+#pragma unroll
+  for (uint32_t r = 0; r < kQPT; ++r) {
+    const uint64_t i = i0 + (uint64_t)r * kBlk;
+    fq[r] = i < n ? fid[i] : kSentinel;
+  }
   for (uint32_t f = threadIdx.x; f <= F; f += kBlk) {
     lh[f] = 0;
     if (f < F) ltiles[f] = desc[f].tiles;
   }
   __syncthreads();
-  const uint64_t i0 = (uint64_t)blockIdx.x * kQB + threadIdx.x;
 #pragma unroll
-  for (uint32_t r = 0; r < kQPT; ++r) {
-    const uint64_t i = i0 + (uint64_t)r * kBlk;
-    if (i < n) atomicAdd(&lh[bucket_of(fid[i], F, ltiles)], 1u);
-  }
+  for (uint32_t r = 0; r < kQPT; ++r)
+    if (i0 + (uint64_t)r * kBlk < n) atomicAdd(&lh[bucket_of(fq[r], F, ltiles)], 1u);
   __syncthreads();
-  for (uint32_t f = threadIdx.x; f <= F; f += kBlk) hist[(uint64_t)f * nb + blockIdx.x] = lh[f];
+  // block-major: this block's F+1 counts are one contiguous row
+  for (uint32_t f = threadIdx.x; f <= F; f += kBlk) hist[(uint64_t)blockIdx.x * (F + 1) + f] = lh[f];
 }
 
 // ---------------------------------------------------------------- K2
-__global__ __launch_bounds__(256) void pb_rows_kernel(const uint32_t *__restrict__ hist, uint32_t nb,
+__global__ __launch_bounds__(256) void pb_rows_kernel(const uint32_t *__restrict__ hist, uint32_t nb, uint32_t F,
                                                       PFilter *__restrict__ desc) {
   __shared__ uint32_t red[256];
   const uint32_t f = blockIdx.x;
   uint32_t s = 0;
-  for (uint32_t b = threadIdx.x; b < nb; b += 256) s += hist[(uint64_t)f * nb + b];
+  for (uint32_t b = threadIdx.x; b < nb; b += 256) s += hist[(uint64_t)b * (F + 1) + f];
   red[threadIdx.x] = s;
   __syncthreads();
   for (uint32_t h = 128; h; h >>= 1) {
@@ -192,20 +203,21 @@ __device__ __forceinline__ uint64_t block_sum64(uint64_t v, uint64_t *red) {
   return t;
 }
 
-__global__ __launch_bounds__(kBlk) void pb_scan_kernel(uint32_t *__restrict__ hist, uint32_t nb, uint32_t F,
-                                                       uint32_t C, uint64_t maxch, PFilter *__restrict__ desc,
-                                                       uint32_t *__restrict__ chunk_filter, uint32_t *__restrict__ scal) {
+__global__ __launch_bounds__(kBlk) void pb_scan_kernel(const uint32_t *__restrict__ cnt_, uint32_t *__restrict__ start,
+                                                       uint32_t nb, uint32_t F, uint32_t C, uint64_t maxch,
+                                                       PFilter *__restrict__ desc, uint32_t *__restrict__ chunk_filter,
+                                                       uint32_t *__restrict__ scal) {
   __shared__ uint64_t red[kBlk / kWave];
   __shared__ uint32_t scratch[kBlk / kWave + 1];
   const uint32_t f = blockIdx.x;
   // sums over the filters before f: queries, chunks, table entries
   uint64_t sq = 0, sc = 0, st = 0;
   for (uint32_t g = threadIdx.x; g < f; g += kBlk) {
-    const PFilter d = desc[g];
-    const uint32_t nc = (d.cnt + C - 1) / C;
-    sq += d.cnt;
+    const uint32_t cg = desc[g].cnt, tg = desc[g].tiles;
+    const uint32_t nc = (cg + C - 1) / C;
+    sq += cg;
     sc += nc;
-    st += (uint64_t)(d.tiles + 1) * nc;
+    st += (uint64_t)(tg + 1) * nc;
   }
   sq = block_sum64(sq, red);
   sc = block_sum64(sc, red);
@@ -225,175 +237,323 @@ __global__ __launch_bounds__(kBlk) void pb_scan_kernel(uint32_t *__restrict__ hi
   // row f: block b's first slot in filter f's run
   const uint32_t per = (nb + kBlk - 1) / kBlk;
   const uint32_t b0 = threadIdx.x * per, b1 = min(b0 + per, nb);
-  uint32_t *row = hist + (uint64_t)f * nb;
+  const uint64_t stride = F + 1;  // block-major: column f
   uint32_t s = 0;
-  for (uint32_t b = b0; b < b1; ++b) s += row[b];
+  for (uint32_t b = b0; b < b1; ++b) s += cnt_[b * stride + f];
   uint32_t total;
   uint32_t run = (uint32_t)sq + block_excl_scan<kBlk>(s, scratch, &total);
   for (uint32_t b = b0; b < b1; ++b) {
-    const uint32_t v = row[b];
-    row[b] = run;
-    run += v;
+    start[b * stride + f] = run;
+    run += cnt_[b * stride + f];
   }
+}
+
+// A block's runs: filter f's queries of block b go to slots [lstart[f],
+// lstart[f] + lcnt[f]) in filter order and to places [lbase[f], ...) of the
+// block's own sorted order.  Loads lcnt, lstart (and ltiles) and scans lbase.
+__device__ __forceinline__ void load_runs(const uint32_t *cnt, const uint32_t *start, uint32_t nb, uint32_t F,
+                                          const PFilter *desc, uint32_t *lcnt, uint32_t *lstart, uint32_t *lbase,
+                                          uint32_t *ltiles, uint32_t *scratch) {
+  const uint64_t row = (uint64_t)blockIdx.x * (F + 1);  // block-major
+  for (uint32_t f = threadIdx.x; f <= F; f += kBlk) {
+    const uint32_t c = cnt[row + f];
+    lcnt[f] = c;
+    lbase[f] = c;
+    lstart[f] = start[row + f];
+    if (ltiles && f < F) ltiles[f] = desc[f].tiles;
+  }
+  __syncthreads();
+  block_excl_scan_array<kBlk>(lbase, F + 1, scratch);
 }
 
 // ---------------------------------------------------------------- K3
 __global__ __launch_bounds__(kBlk) void pb_scatter_kernel(const uint4 *__restrict__ keys,
                                                           const uint32_t *__restrict__ fid, uint64_t n, uint32_t F,
                                                           uint32_t nb, const PFilter *__restrict__ desc,
-                                                          const uint32_t *__restrict__ hist,
-                                                          uint32_t *__restrict__ dest, uint2 *__restrict__ hs) {
-  extern __shared__ uint32_t lds[];
-  uint32_t *cur = lds, *ltiles = lds + F + 1;
-  for (uint32_t f = threadIdx.x; f <= F; f += kBlk) {
-    cur[f] = hist[(uint64_t)f * nb + blockIdx.x];
-    if (f < F) ltiles[f] = desc[f].tiles;
-  }
+                                                          const uint32_t *__restrict__ cnt,
+                                                          const uint32_t *__restrict__ start,
+                                                          uint16_t *__restrict__ dest, uint2 *__restrict__ hs) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  uint2 *lhs = reinterpret_cast<uint2 *>(lds);  // kQB hashes in the block's filter order
+  uint32_t *lcnt = lds + 2 * kQB, *lstart = lcnt + F + 1, *lbase = lstart + F + 1, *lcur = lbase + F + 1;
+  uint32_t *ltiles = lcur + F + 1, *scratch = ltiles + F + 1;
+  const int tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid / kWave;
+  load_runs(cnt, start, nb, F, desc, lcnt, lstart, lbase, ltiles, scratch);
+  for (uint32_t f = tid; f <= F; f += kBlk) lcur[f] = lbase[f];
   __syncthreads();
-  const uint64_t i0 = (uint64_t)blockIdx.x * kQB + threadIdx.x;
+  const uint64_t i0 = (uint64_t)blockIdx.x * kQB + tid;
 #pragma unroll 4
   for (uint32_t r = 0; r < kQPT; ++r) {
     const uint64_t i = i0 + (uint64_t)r * kBlk;
     if (i < n) {
       const uint32_t b = bucket_of(fid[i], F, ltiles);
+      uint16_t place = kNoSlot;
       if (b < F) {
-        const uint32_t d = atomicAdd(&cur[b], 1u);
+        place = (uint16_t)atomicAdd(&lcur[b], 1u);
         uint32_t h1, h2;
         hash16(load_nt(keys + i), h1, h2);
-        hs[d] = make_uint2(h1, h2);
-        dest[i] = d;
-      } else {
-        dest[i] = kSentinel;
+        lhs[place] = make_uint2(h1, h2);
       }
+      dest[i] = place;
     }
+  }
+  __syncthreads();
+  // run by run: consecutive lanes write consecutive slots (whole lines)
+  for (uint32_t f = wave; f < F; f += kBlk / kWave) {
+    const uint32_t c = lcnt[f], lb = lbase[f], gs = lstart[f];
+    for (uint32_t r = lane; r < c; r += kWave) hs[gs + r] = lhs[lb + r];
   }
 }
 
 // ---------------------------------------------------------------- P1
+// Persistent: workgroup b takes chunks b, b + G, ...; the next chunk's hashes
+// are in flight into registers while the current one is sorted and stored.
 template <int KFIX>
 __global__ __launch_bounds__(kBlk) void pb_bin_kernel(const uint2 *__restrict__ hs, const PFilter *__restrict__ desc,
-                                                      const uint32_t *__restrict__ chunk_filter, uint32_t k,
-                                                      uint32_t C, uint32_t *__restrict__ ent,
-                                                      uint32_t *__restrict__ table, uint8_t *__restrict__ res) {
+                                                      const uint32_t *__restrict__ chunk_filter,
+                                                      const uint32_t *__restrict__ scal, uint32_t k, uint32_t C,
+                                                      uint32_t *__restrict__ ent, uint32_t *__restrict__ table,
+                                                      uint8_t *__restrict__ res) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   uint32_t *hist = lds;                          // kMaxTiles + 1 counters, later cursors
   uint32_t *scratch = lds + kMaxTiles + 4;       // scan scratch (64 words)
   uint32_t *lpos = scratch + 64;                 // k*C sorted entries
-  const uint32_t f = chunk_filter[blockIdx.x];
-  if (f == kSentinel) return;  // past the last chunk
-  const PFilter d = desc[f];
-  const uint32_t j = blockIdx.x - d.chunk_base;
-  const uint32_t q0 = d.qbase + j * C;
-  const uint32_t cnt = min(C, d.cnt - j * C);
-  const uint32_t T = d.tiles;
-  const FastMod mod{d.m, d.magic, d.shift, 0u};
   const uint32_t kk = KFIX > 0 ? (uint32_t)KFIX : k;
+  constexpr int KR = KFIX > 0 ? KFIX : 1;
   const int tid = threadIdx.x;
-  for (uint32_t t = tid; t <= T; t += kBlk) hist[t] = 0;
-  uint32_t h1[kCPT], h2[kCPT];
+  const uint32_t total_chunks = scal[1];
+  const uint32_t G = gridDim.x;
+  auto fetch = [&](uint32_t c, uint2 (&h)[kCPT]) {
+    if (c >= total_chunks) return;
+    const uint32_t f = chunk_filter[c];
+    const uint32_t j = c - desc[f].chunk_base;
+    const uint32_t q0 = desc[f].qbase + j * C;
+    const uint32_t cnt = min(C, desc[f].cnt - j * C);
 #pragma unroll
-  for (uint32_t r = 0; r < kCPT; ++r) {
-    const uint32_t q = tid + r * kBlk;
-    h1[r] = h2[r] = 0;
-    if (q < cnt) {
-      const uint2 h = hs[q0 + q];
-      h1[r] = h.x;
-      h2[r] = h.y;
-      res[q0 + q] = 1;
+    for (uint32_t r = 0; r < kCPT; ++r) {
+      const uint32_t q = tid + r * kBlk;
+      h[r] = hs[q0 + min(q, cnt - 1u)];
     }
-  }
-  __syncthreads();
+  };
+  uint2 nxt[kCPT];
+  fetch(blockIdx.x, nxt);
+  for (uint32_t c = blockIdx.x; c < total_chunks; c += G) {
+    uint2 cur[kCPT];
 #pragma unroll
-  for (uint32_t r = 0; r < kCPT; ++r) {
-    if (tid + r * kBlk < cnt) {
-      for (uint32_t jj = 0; jj < kk; ++jj) atomicAdd(&hist[fastmod(h1[r] + jj * h2[r], mod) >> kTL], 1u);
-    }
-  }
-  __syncthreads();
-  const uint32_t total = block_excl_scan_array<kBlk>(hist, T + 1, scratch);
-  uint32_t *tab = table + d.table_base;
-  for (uint32_t t = tid; t <= T; t += kBlk) tab[(uint64_t)t * d.nchunks + j] = hist[t];
-  __syncthreads();
+    for (uint32_t r = 0; r < kCPT; ++r) cur[r] = nxt[r];
+    fetch(c + G, nxt);
+    const uint32_t f = chunk_filter[c];
+    const PFilter d = desc[f];
+    const uint32_t j = c - d.chunk_base;
+    const uint32_t q0 = d.qbase + j * C;
+    const uint32_t cnt = min(C, d.cnt - j * C);
+    const uint32_t T = d.tiles;
+    const FastMod mod{d.m, d.magic, d.shift, 0u};
+    __syncthreads();  // the previous chunk's entries are read out of lpos
+    for (uint32_t t = tid; t <= T; t += kBlk) hist[t] = 0;
 #pragma unroll
-  for (uint32_t r = 0; r < kCPT; ++r) {
-    const uint32_t q = tid + r * kBlk;
-    if (q < cnt) {
-      for (uint32_t jj = 0; jj < kk; ++jj) {
-        const uint32_t p = fastmod(h1[r] + jj * h2[r], mod);
-        const uint32_t slot = atomicAdd(&hist[p >> kTL], 1u);
-        lpos[slot] = (q << kTL) | (p & ((1u << kTL) - 1u));
+    for (uint32_t r = 0; r < kCPT; ++r)
+      if (tid + r * kBlk < cnt) res[q0 + tid + r * kBlk] = 1;
+    __syncthreads();
+    uint32_t pos[kCPT][KR];
+#pragma unroll
+    for (uint32_t r = 0; r < kCPT; ++r) {
+      if (tid + r * kBlk < cnt) {
+        if constexpr (KFIX > 0) {
+#pragma unroll
+          for (int jj = 0; jj < KFIX; ++jj) {
+            pos[r][jj] = fastmod(cur[r].x + (uint32_t)jj * cur[r].y, mod);
+            atomicAdd(&hist[pos[r][jj] >> kTL], 1u);
+          }
+        } else {
+          for (uint32_t jj = 0; jj < kk; ++jj) atomicAdd(&hist[fastmod(cur[r].x + jj * cur[r].y, mod) >> kTL], 1u);
+        }
       }
     }
+    __syncthreads();
+    const uint32_t total = block_excl_scan_array<kBlk>(hist, T + 1, scratch);
+    uint32_t *tab = table + d.table_base;
+    for (uint32_t t = tid; t <= T; t += kBlk) tab[(uint64_t)t * d.nchunks + j] = hist[t];
+    __syncthreads();
+#pragma unroll
+    for (uint32_t r = 0; r < kCPT; ++r) {
+      const uint32_t q = tid + r * kBlk;
+      if (q < cnt) {
+        if constexpr (KFIX > 0) {
+          uint32_t sl[KFIX];
+#pragma unroll
+          for (int jj = 0; jj < KFIX; ++jj) sl[jj] = atomicAdd(&hist[pos[r][jj] >> kTL], 1u);
+#pragma unroll
+          for (int jj = 0; jj < KFIX; ++jj) lpos[sl[jj]] = (q << kTL) | (pos[r][jj] & ((1u << kTL) - 1u));
+        } else {
+          for (uint32_t jj = 0; jj < kk; ++jj) {
+            const uint32_t p = fastmod(cur[r].x + jj * cur[r].y, mod);
+            const uint32_t slot = atomicAdd(&hist[p >> kTL], 1u);
+            lpos[slot] = (q << kTL) | (p & ((1u << kTL) - 1u));
+          }
+        }
+      }
+    }
+    __syncthreads();
+    uint32_t *dst = ent + (uint64_t)c * k * C;
+    const uint32_t nvec = total >> 2;
+    const uint4 *src4 = reinterpret_cast<const uint4 *>(lpos);
+    uint4 *dst4 = reinterpret_cast<uint4 *>(dst);
+    for (uint32_t v = tid; v < nvec; v += kBlk) dst4[v] = src4[v];
+    for (uint32_t v = (nvec << 2) + tid; v < total; v += kBlk) dst[v] = lpos[v];
   }
-  __syncthreads();
-  uint32_t *dst = ent + (uint64_t)blockIdx.x * k * C;
-  const uint32_t nvec = total >> 2;
-  const uint4 *src4 = reinterpret_cast<const uint4 *>(lpos);
-  uint4 *dst4 = reinterpret_cast<uint4 *>(dst);
-  for (uint32_t v = tid; v < nvec; v += kBlk) dst4[v] = src4[v];
-  for (uint32_t v = (nvec << 2) + tid; v < total; v += kBlk) dst[v] = lpos[v];
 }
 
 // ---------------------------------------------------------------- P2
+// Persistent over the tiles (XCD-consecutive order).  The next tile's bitmap
+// bytes are in flight into registers while the current tile's runs are
+// tested; each wave stages the (start, end) of all its chunks' runs in two
+// registers at the tile's start and keeps two runs' loads in flight.
+constexpr uint32_t kTileVecPT = kTileBytes / 16 / kBlk;  // 16-byte tile vectors per thread
+constexpr int kRunLoads = 6;                             // entries per run per stage: 6 x 64 (runs average ~320)
+
+struct TileRef {
+  uint32_t f, t, sh, nvec, tail;
+  uint64_t a0;
+};
+
+// ltb: the filters' tile_base in LDS (F+1 entries)
+__device__ __forceinline__ TileRef tile_ref(const PFilter *desc, const uint32_t *ltb, uint32_t F, uint32_t g) {
+  uint32_t lo = 0, hi = F;  // the last f with tile_base <= g (tile_base[F] = all tiles > g)
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (ltb[mid] <= g) lo = mid; else hi = mid;
+  }
+  TileRef r;
+  r.f = lo;
+  r.t = g - ltb[lo];
+  const uint64_t base = desc[lo].byte_off;
+  const uint64_t s = base + (uint64_t)r.t * kTileBytes;
+  const uint64_t e = min(s + kTileBytes, base + (uint64_t)(desc[lo].m >> 3));
+  r.a0 = s & ~15ull;
+  r.sh = (uint32_t)(s - r.a0) * 8u;
+  r.nvec = (uint32_t)((e - r.a0) >> 4);
+  r.tail = (uint32_t)(e - r.a0) & 15u;
+  return r;
+}
+
 __global__ __launch_bounds__(kBlk) void pb_tile_kernel(const uint8_t *__restrict__ bitmaps,
                                                        const PFilter *__restrict__ desc, uint32_t F,
                                                        const uint32_t *__restrict__ scal, uint32_t k, uint32_t C,
                                                        const uint32_t *__restrict__ ent,
                                                        const uint32_t *__restrict__ table,
-                                                       uint8_t *__restrict__ res) {
+                                                       uint8_t *__restrict__ res, uint32_t exp) {
+#ifndef ADL_BLOOM_STAMPS
+  exp = 0;  // diagnostics build only (wrong answers): 1 no answer stores, 2 no bitmap loads, 4 no entry loads
+#endif
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-  uint32_t *ltile = lds;  // kTileBytes + 32 bytes: the tile's bitmap bytes from a 16-byte-aligned start
+  uint32_t *ltile = lds;  // the tile's bitmap bytes from a 16-byte-aligned start (+ <= 15 bytes before it)
+  uint32_t *ltb = lds + (kTileBytes + 64) / 4;  // the filters' first tiles (F+1), for the tile -> filter search
   const int tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid / kWave;
   constexpr int NW = kBlk / kWave;
   const uint32_t total_tiles = scal[0];
+  for (uint32_t f = tid; f <= F; f += kBlk) ltb[f] = desc[f].tile_base;
+  __syncthreads();
   const uint32_t G = gridDim.x;
-  // consecutive tiles (whose runs share cache lines in every chunk region)
-  // go to one XCD; speed only
   const uint32_t slot = (G % 8 == 0) ? (blockIdx.x % 8) * (G / 8) + blockIdx.x / 8 : blockIdx.x;
-  for (uint32_t g = slot; g < total_tiles; g += G) {
-    // the filter holding global tile g: the last f with tile_base <= g
-    uint32_t lo = 0, hi = F;  // desc[F].tile_base = total_tiles > g
-    while (hi - lo > 1) {
-      const uint32_t mid = (lo + hi) >> 1;
-      if (desc[mid].tile_base <= g) lo = mid; else hi = mid;
+  uint4 pre[kTileVecPT];
+  auto prefetch = [&](const TileRef &r) {
+    const uint4 *src = reinterpret_cast<const uint4 *>(bitmaps + r.a0);
+#pragma unroll
+    for (uint32_t u = 0; u < kTileVecPT; ++u) {
+      const uint32_t v = tid + u * kBlk;
+      pre[u] = (v < r.nvec && !(exp & 2)) ? load_nt(src + v) : make_uint4(0, 0, 0, 0);
     }
-    const PFilter d = desc[lo];
-    const uint32_t t = g - d.tile_base;
-    // bitmap bytes [s, e) of the tile, staged from a0 = s rounded down to 16
-    const uint64_t s = d.byte_off + (uint64_t)t * kTileBytes;
-    const uint64_t e = min(s + kTileBytes, d.byte_off + (uint64_t)(d.m >> 3));
-    const uint64_t a0 = s & ~15ull;
-    const uint32_t sh = (uint32_t)(s - a0) * 8u;  // bit offset of the tile in ltile
-    const uint32_t nvec = (uint32_t)((e - a0) >> 4);
-    const uint4 *src = reinterpret_cast<const uint4 *>(bitmaps + a0);
-    uint4 *l4 = reinterpret_cast<uint4 *>(ltile);
+  };
+  TileRef cur{};
+  if (slot < total_tiles) {
+    cur = tile_ref(desc, ltb, F, slot);
+    prefetch(cur);
+  }
+  for (uint32_t g = slot; g < total_tiles; g += G) {
     __syncthreads();  // the previous tile's lookups are done
-    for (uint32_t v = tid; v < nvec; v += kBlk) l4[v] = load_nt(src + v);
-    const uint32_t tail = (uint32_t)(e - a0) & 15u;
-    if ((uint32_t)tid < tail)
-      reinterpret_cast<uint8_t *>(ltile)[nvec * 16 + tid] = bitmaps[a0 + nvec * 16 + tid];
-    __syncthreads();
-    // every chunk's run for this tile: wave w takes chunks w, w + 16, ...
+    uint4 *l4 = reinterpret_cast<uint4 *>(ltile);
+#pragma unroll
+    for (uint32_t u = 0; u < kTileVecPT; ++u) {
+      const uint32_t v = tid + u * kBlk;
+      if (v < cur.nvec) l4[v] = pre[u];
+    }
+    if ((uint32_t)tid < cur.tail)
+      reinterpret_cast<uint8_t *>(ltile)[cur.nvec * 16 + tid] = bitmaps[cur.a0 + cur.nvec * 16 + tid];
+    const TileRef now = cur;
+    if (g + G < total_tiles) {
+      cur = tile_ref(desc, ltb, F, g + G);
+      prefetch(cur);
+    }
+    const PFilter d = desc[now.f];
     const uint32_t nc = d.nchunks;
-    const uint32_t *row = table + d.table_base + (uint64_t)t * nc;
-    for (uint32_t jc = wave; jc < nc; jc += NW) {
-      const uint32_t b0 = __builtin_amdgcn_readfirstlane(row[jc]);
-      const uint32_t b1 = __builtin_amdgcn_readfirstlane(row[nc + jc]);
+    const uint32_t *row = table + d.table_base + (uint64_t)now.t * nc;
+    // this wave's runs: chunks wave + NW*q; lane q holds run q's (start, end)
+    const uint32_t nq = nc > (uint32_t)wave ? (nc - wave + NW - 1) / NW : 0u;
+    __syncthreads();  // the tile is in LDS
+    // two-stage pipeline over the wave's runs: run q+1's first 8 x 64
+    // entries are in flight while run q is tested
+    struct Stage {
+      uint32_t x[kRunLoads];
+      uint32_t b0, b1, jc;
+    };
+    auto issue = [&](Stage &sg, uint32_t b0, uint32_t b1, uint32_t jc) {
+      sg.b0 = b0;
+      sg.b1 = b1;
+      sg.jc = jc;
       const uint32_t *run = ent + (uint64_t)(d.chunk_base + jc) * k * C;
-      uint8_t *rq = res + d.qbase + (uint64_t)jc * C;
-      for (uint32_t o = b0; o < b1; o += 4 * kWave) {
-        uint32_t x[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const uint32_t idx = o + u * kWave + lane;
-          x[u] = idx < b1 ? run[idx] : 0u;
-        }
+      for (int u = 0; u < kRunLoads; ++u) {
+        const uint32_t idx = b0 + u * kWave + lane;
+        // an empty run reads entry b0-1: inside the workspace, unused
+        sg.x[u] = (exp & 4) ? (idx * 2654435761u) & 0x7fffffu : run[min(idx, b1 - 1u)];
+      }
+    };
+    // 8 entries per lane: all 8 LDS words are read before any is tested (the
+    // reads are unconditional -- a lane past the run holds a clamped entry of
+    // it -- so they issue back to back), then the clear bits store 0
+    auto test8 = [&](const uint32_t (&x)[kRunLoads], uint32_t o, uint32_t b1, uint8_t *rq) {
+      uint32_t w[kRunLoads];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          if (o + u * kWave + lane < b1) {
-            const uint32_t bit = (x[u] & ((1u << kTL) - 1u)) + sh;
-            if (!((ltile[bit >> 5] >> (bit & 31)) & 1u)) rq[x[u] >> kTL] = 0;
-          }
+      for (int u = 0; u < kRunLoads; ++u) w[u] = ltile[((x[u] & ((1u << kTL) - 1u)) + now.sh) >> 5];
+#pragma unroll
+      for (int u = 0; u < kRunLoads; ++u) {
+        const uint32_t bit = (x[u] & ((1u << kTL) - 1u)) + now.sh;
+        if (o + u * kWave + lane < b1 && !((w[u] >> (bit & 31)) & 1u) && !(exp & 1)) rq[x[u] >> kTL] = 0;
+      }
+    };
+    auto consume = [&](const Stage &sg) {
+      uint8_t *rq = res + d.qbase + (uint64_t)sg.jc * C;
+      test8(sg.x, sg.b0, sg.b1, rq);
+      // a run longer than 8 x 64 entries (few tiles per filter): the rest
+      const uint32_t *run = ent + (uint64_t)(d.chunk_base + sg.jc) * k * C;
+      for (uint32_t o = sg.b0 + kRunLoads * kWave; o < sg.b1; o += kRunLoads * kWave) {
+        uint32_t x[kRunLoads];
+#pragma unroll
+        for (int u = 0; u < kRunLoads; ++u) x[u] = run[min(o + u * kWave + lane, sg.b1 - 1u)];
+        test8(x, o, sg.b1, rq);
+      }
+    };
+    for (uint32_t q0 = 0; q0 < nq; q0 += kWave) {
+      uint32_t rs = 0, re = 0;
+      if (q0 + lane < nq) {
+        const uint32_t jc = wave + NW * (q0 + lane);
+        rs = row[jc];
+        re = row[nc + jc];
+      }
+      const uint32_t nr = min((uint32_t)kWave, nq - q0);
+      Stage A, B;
+      issue(A, __builtin_amdgcn_readlane(rs, 0), __builtin_amdgcn_readlane(re, 0), wave + NW * q0);
+      for (uint32_t q = 0; q < nr; q += 2) {
+        if (q + 1 < nr)
+          issue(B, __builtin_amdgcn_readlane(rs, q + 1), __builtin_amdgcn_readlane(re, q + 1),
+                wave + NW * (q0 + q + 1));
+        consume(A);
+        if (q + 1 < nr) {
+          if (q + 2 < nr)
+            issue(A, __builtin_amdgcn_readlane(rs, q + 2), __builtin_amdgcn_readlane(re, q + 2),
+                  wave + NW * (q0 + q + 2));
+          consume(B);
         }
       }
     }
@@ -401,12 +561,52 @@ __global__ __launch_bounds__(kBlk) void pb_tile_kernel(const uint8_t *__restrict
 }
 
 // ---------------------------------------------------------------- K6
-__global__ __launch_bounds__(256) void pb_gather_kernel(const uint32_t *__restrict__ dest,
-                                                        const uint8_t *__restrict__ res, uint64_t n,
-                                                        uint8_t *__restrict__ out) {
-  for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
-    const uint32_t dd = dest[i];
-    out[i] = dd == kSentinel ? 0 : res[dd];
+__global__ __launch_bounds__(kBlk) void pb_gather_kernel(const uint16_t *__restrict__ dest,
+                                                         const uint8_t *__restrict__ res, uint64_t n, uint32_t F,
+                                                         uint32_t nb, const uint32_t *__restrict__ cnt,
+                                                         const uint32_t *__restrict__ start,
+                                                         uint8_t *__restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  uint8_t *lres = reinterpret_cast<uint8_t *>(lds);  // kQB answers in the block's filter order
+  uint32_t *lcnt = lds + kQB / 4, *lstart = lcnt + F + 1, *lbase = lstart + F + 1, *scratch = lbase + F + 1;
+  const int tid = threadIdx.x;
+  // this thread's queries' places: in flight while the block's runs are set up
+  const uint64_t i0 = (uint64_t)blockIdx.x * kQB + tid;
+  uint16_t pl_q[kQPT];
+#pragma unroll
+  for (uint32_t r = 0; r < kQPT; ++r) {
+    const uint64_t i = i0 + (uint64_t)r * kBlk;
+    pl_q[r] = i < n ? dest[i] : kNoSlot;
+  }
+  load_runs(cnt, start, nb, F, nullptr, lcnt, lstart, lbase, nullptr, scratch);
+  // place p of the block's sorted order belongs to the filter whose run holds
+  // it (the last f with lbase[f] <= p, runs of the same filter are
+  // contiguous); all kQPT loads of a thread are in flight together
+  const uint32_t nvalid = lbase[F];
+  uint8_t v[kQPT];
+#pragma unroll
+  for (uint32_t r = 0; r < kQPT; ++r) {
+    const uint32_t pl = tid + r * kBlk;
+    v[r] = 0;
+    if (pl < nvalid) {
+      uint32_t lo = 0, hi = F;  // lbase[lo] <= pl < lbase[hi]
+      while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (lbase[mid] <= pl) lo = mid; else hi = mid;
+      }
+      v[r] = res[lstart[lo] + (pl - lbase[lo])];
+    }
+  }
+#pragma unroll
+  for (uint32_t r = 0; r < kQPT; ++r) {
+    const uint32_t pl = tid + r * kBlk;
+    if (pl < nvalid) lres[pl] = v[r];
+  }
+  __syncthreads();
+#pragma unroll
+  for (uint32_t r = 0; r < kQPT; ++r) {
+    const uint64_t i = i0 + (uint64_t)r * kBlk;
+    if (i < n) out[i] = pl_q[r] == kNoSlot ? 0 : lres[pl_q[r]];
   }
 }
 
@@ -448,40 +648,50 @@ int adl_bloom_probe_batch_device(const uint8_t *d_keys, const uint64_t *d_offset
   uint8_t *ws = reinterpret_cast<uint8_t *>(adl_host::round_up(reinterpret_cast<uintptr_t>(d_workspace), 256));
   PFilter *desc = reinterpret_cast<PFilter *>(ws + p.o_desc);
   uint32_t *scal = reinterpret_cast<uint32_t *>(ws + p.o_scal);
-  uint32_t *hist = reinterpret_cast<uint32_t *>(ws + p.o_hist);
+  uint32_t *cnt = reinterpret_cast<uint32_t *>(ws + p.o_cnt);
+  uint32_t *start = reinterpret_cast<uint32_t *>(ws + p.o_start);
   uint32_t *cf = reinterpret_cast<uint32_t *>(ws + p.o_cf);
-  uint32_t *dest = reinterpret_cast<uint32_t *>(ws + p.o_dest);
+  uint16_t *dest = reinterpret_cast<uint16_t *>(ws + p.o_dest);
   uint2 *hs = reinterpret_cast<uint2 *>(ws + p.o_hs);
   uint32_t *ent = reinterpret_cast<uint32_t *>(ws + p.o_ent);
   uint32_t *tab = reinterpret_cast<uint32_t *>(ws + p.o_tab);
   uint8_t *res = ws + p.o_res;
   const uint32_t F = num_filters;
-  const size_t lds_b = (size_t)(2 * F + 2) * 4;  // K1 / K3: F+1 counters + F tile counts
+  const uint32_t cus = adl_host::device_cus();
+  const size_t lds_k1 = (size_t)(2 * F + 2) * 4;                       // counters + tile counts
+  const size_t lds_k3 = (size_t)(2 * kQB + 5 * (F + 1) + 32) * 4;      // hashes + 5 per-filter arrays + scratch
+  const size_t lds_k6 = (size_t)(kQB / 4 + 3 * (F + 1) + 32) * 4;      // answers + 3 per-filter arrays + scratch
+  const size_t lds_p1 = (size_t)(kMaxTiles + 4 + 64 + p.k * p.C) * 4;
+  const size_t lds_p2 = (size_t)kTileBytes + 64 + (size_t)(F + 1) * 4;
   try {
     hipLaunchKernelGGL(pb_desc_kernel, dim3(1), dim3(kBlk), 0, st, d_bitmap_off, d_bitmap_end, F, desc, scal);
     ADL_HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(pb_hist_kernel, dim3(p.nb), dim3(kBlk), lds_b, st, d_filter_id, n, F, p.nb, desc, hist);
+    hipLaunchKernelGGL(pb_hist_kernel, dim3(p.nb), dim3(kBlk), lds_k1, st, d_filter_id, n, F, p.nb, desc, cnt);
     ADL_HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(pb_rows_kernel, dim3(F + 1), dim3(256), 0, st, hist, p.nb, desc);
+    hipLaunchKernelGGL(pb_rows_kernel, dim3(F + 1), dim3(256), 0, st, cnt, p.nb, F, desc);
     ADL_HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(pb_scan_kernel, dim3(F + 1), dim3(kBlk), 0, st, hist, p.nb, F, p.C, p.maxch, desc, cf, scal);
+    hipLaunchKernelGGL(pb_scan_kernel, dim3(F + 1), dim3(kBlk), 0, st, cnt, start, p.nb, F, p.C, p.maxch, desc, cf,
+                       scal);
     ADL_HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(pb_scatter_kernel, dim3(p.nb), dim3(kBlk), lds_b, st, reinterpret_cast<const uint4 *>(d_keys),
-                       d_filter_id, n, F, p.nb, desc, hist, dest, hs);
+    ADL_HIP_TRY(hipFuncSetAttribute((const void *)pb_scatter_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)lds_k3));
+    hipLaunchKernelGGL(pb_scatter_kernel, dim3(p.nb), dim3(kBlk), lds_k3, st, reinterpret_cast<const uint4 *>(d_keys),
+                       d_filter_id, n, F, p.nb, desc, cnt, start, dest, hs);
     ADL_HIP_TRY(hipGetLastError());
-    const size_t lds_p1 = (size_t)(kMaxTiles + 4 + 64 + p.k * p.C) * 4;
     auto p1 = p.k == 6 ? pb_bin_kernel<6> : pb_bin_kernel<0>;
     ADL_HIP_TRY(hipFuncSetAttribute((const void *)p1, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_p1));
-    hipLaunchKernelGGL(p1, dim3((uint32_t)p.maxch), dim3(kBlk), lds_p1, st, hs, desc, cf, p.k, p.C, ent, tab, res);
+    hipLaunchKernelGGL(p1, dim3(cus), dim3(kBlk), lds_p1, st, hs, desc, cf, scal, p.k, p.C, ent, tab, res);
     ADL_HIP_TRY(hipGetLastError());
-    const size_t lds_p2 = (size_t)kTileBytes + 64;
     ADL_HIP_TRY(hipFuncSetAttribute((const void *)pb_tile_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     (int)lds_p2));
-    hipLaunchKernelGGL(pb_tile_kernel, dim3(adl_host::device_cus()), dim3(kBlk), lds_p2, st, d_bitmaps, desc, F,
-                       scal, p.k, p.C, ent, tab, res);
+    const char *exp_env = getenv("ADL_PB_EXP");  // diagnostics build only
+    hipLaunchKernelGGL(pb_tile_kernel, dim3(cus), dim3(kBlk), lds_p2, st, d_bitmaps, desc, F, scal, p.k, p.C, ent,
+                       tab, res, exp_env ? (uint32_t)atoi(exp_env) : 0u);
     ADL_HIP_TRY(hipGetLastError());
-    const uint32_t g6 = (uint32_t)std::min<uint64_t>((n + 255) / 256, (uint64_t)adl_host::device_cus() * 16);
-    hipLaunchKernelGGL(pb_gather_kernel, dim3(g6), dim3(256), 0, st, dest, res, n, d_out);
+    ADL_HIP_TRY(hipFuncSetAttribute((const void *)pb_gather_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)lds_k6));
+    hipLaunchKernelGGL(pb_gather_kernel, dim3(p.nb), dim3(kBlk), lds_k6, st, dest, res, n, F, p.nb, cnt, start,
+                       d_out);
     ADL_HIP_TRY(hipGetLastError());
     return ADL_OK;
   } catch (...) {

@@ -85,17 +85,20 @@ def test_config3_compaction_256_tables(arena, pins):
     assert not bad, f"tables {bad[:10]} differ from the oracle"
 
 
-def test_config4_probe_100m(dev, ab, arena, pins):
+@pytest.mark.parametrize("path", ["direct", "batch"])
+def test_config4_probe_100m(dev, ab, arena, pins, path):
+    """direct: bloom_probe_multi_kernel; batch: adl_bloom_probe_batch_device, the
+    tile-binned pipeline at this size (bench.py's probe step)."""
     p = pins["probe"]
     packed, off = arena
     d_off = dev.from_numpy(off.view(np.int64)).cuda()
     h = hashlib.sha256()
     n_ins = hits = fps = 0
-    step = 25_000_000
+    step = 25_000_000 if path == "direct" else p["queries"]
     for q0 in range(0, p["queries"], step):
         k, f, m = ab.synth_probe_queries(min(step, p["queries"] - q0), seed=p["seed"], q0=q0,
                                          num_tables=p["tables"], keys_per_table=p["keys_per_table"])
-        r = ab.probe_multi(k, f, packed, d_off)
+        r = (ab.probe_multi if path == "direct" else ab.probe_batch)(k, f, packed, d_off)
         rh, mh = r.cpu().numpy(), m.cpu().numpy()
         h.update(rh.tobytes())
         n_ins += int(mh.sum())
