@@ -20,8 +20,8 @@ from collections import defaultdict
 
 root, out, workload = sys.argv[1], sys.argv[2], sys.argv[3]
 launches_per_step = float(sys.argv[4]) if len(sys.argv) > 4 else 1.0
-KERNELS = ("bloom_bin", "bloom_tile", "bloom_probe_multi", "bloom_probe_tile", "bloom_probe_bin",
-           "bloom_probe_sort", "bloom_probe_gather")
+KERNELS = ("bloom_bin", "bloom_tile", "bloom_probe_multi", "pb_desc", "pb_hist", "pb_rows", "pb_scan",
+           "pb_scatter", "pb_bin", "pb_tile", "pb_gather")
 acc = defaultdict(lambda: defaultdict(list))
 for f in glob.glob(os.path.join(root, "p*", "**", "*counter_collection.csv"), recursive=True):
     for row in csv.DictReader(open(f)):
@@ -46,6 +46,9 @@ for kern, cs in acc.items():
 d = {}
 if os.path.exists(out):
     d = json.load(open(out))
+if workload == "probe":  # the probe step is the pb_* pipeline; the builds in its setup are not part of it
+    per = {k: v for k, v in per.items() if k.startswith("pb_") or k == "bloom_probe_multi"}
+    total = sum(v["hbm_bytes"] for v in per.values())
 d[workload] = {"hbm_bytes_per_build": round(total), "per_kernel": per,
                "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes; reads x2 (gfx950)"}
 json.dump(d, open(out, "w"), indent=1)
