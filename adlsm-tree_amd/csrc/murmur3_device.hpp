@@ -39,6 +39,9 @@ __device__ __forceinline__ uint32_t rotl_quirk(uint32_t x) {
 
 __device__ __forceinline__ uint32_t mix_block(uint32_t h, uint32_t k) {
   k *= 0xcc9e2d51u;       // :31
+  // opaque: otherwise the compiler folds the rotate's k << 15 into a second
+  // v_mul_lo_u32 by c1 << 15 (a quarter-rate op for a full-rate shift)
+  asm("" : "+v"(k));
   k = rotl_quirk<15>(k);  // :32
   k *= 0x1b873593u;       // :33
   h ^= k;                 // :35
@@ -143,7 +146,23 @@ __device__ __forceinline__ void hash_lds(const uint32_t *stage, uint32_t off, ui
   const uint32_t nblk = len >> 2, sh = off & 3u;
   uint32_t wi = off >> 2;
   uint32_t lo = stage[wi];
-  for (uint32_t i = 0; i < nblk; ++i) {
+  uint32_t i = 0;
+  // four blocks per step: their four LDS words are read before the first is
+  // mixed, so one LDS round trip covers 16 key bytes
+  for (; i + 4 <= nblk; i += 4) {
+    uint32_t w[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) w[u] = stage[wi + 1 + u];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint32_t q = quirk_word(__builtin_amdgcn_alignbyte(w[u], u ? w[u - 1] : lo, sh));
+      a = mix_block(a, q);
+      b = mix_block(b, q);
+    }
+    lo = w[3];
+    wi += 4;
+  }
+  for (; i < nblk; ++i) {
     const uint32_t hi = stage[++wi];
     const uint32_t q = quirk_word(__builtin_amdgcn_alignbyte(hi, lo, sh));
     a = mix_block(a, q);
