@@ -21,10 +21,13 @@
  *
  * Every function returns an adl_status (0 = OK).  All entry points are
  * re-entrant and thread-safe: work is enqueued on the caller's HIP stream
- * (`stream`, a hipStream_t; NULL = the null stream) and nothing global is
- * mutated after the once-guarded device query.  Functions named *_device take
- * device pointers and do not synchronise; the others take host pointers and
- * return when the results are in host memory.
+ * (`stream`, a hipStream_t) and nothing global is mutated after the
+ * once-guarded device query.  Functions named *_device take device pointers
+ * and do not synchronise; there NULL = the null stream.  The others take host
+ * pointers and return when the results are in host memory; there NULL = a
+ * non-blocking stream of the calling thread (created on first use), so calls
+ * from different threads run side by side on the device instead of queueing
+ * on the legacy null stream.
  */
 #ifndef ADL_BLOOM_H_
 #define ADL_BLOOM_H_
