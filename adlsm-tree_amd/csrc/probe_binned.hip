@@ -278,20 +278,31 @@ __global__ __launch_bounds__(kBlk) void pb_scatter_kernel(const uint4 *__restric
   uint32_t *lcnt = lds + 2 * kQB, *lstart = lcnt + F + 1, *lbase = lstart + F + 1, *lcur = lbase + F + 1;
   uint32_t *ltiles = lcur + F + 1, *scratch = ltiles + F + 1;
   const int tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid / kWave;
+  // every query's id and key are requested first (unconditionally: a lane
+  // past n loads the last query and discards it), so they land while the
+  // block's runs are set up
+  const uint64_t i0 = (uint64_t)blockIdx.x * kQB + tid;
+  uint32_t fq[kQPT];
+  uint4 kq[kQPT];
+#pragma unroll
+  for (uint32_t r = 0; r < kQPT; ++r) {
+    const uint64_t i = min(i0 + (uint64_t)r * kBlk, n - 1);
+    fq[r] = fid[i];
+    kq[r] = load_nt(keys + i);
+  }
   load_runs(cnt, start, nb, F, desc, lcnt, lstart, lbase, ltiles, scratch);
   for (uint32_t f = tid; f <= F; f += kBlk) lcur[f] = lbase[f];
   __syncthreads();
-  const uint64_t i0 = (uint64_t)blockIdx.x * kQB + tid;
-#pragma unroll 4
+#pragma unroll
   for (uint32_t r = 0; r < kQPT; ++r) {
     const uint64_t i = i0 + (uint64_t)r * kBlk;
     if (i < n) {
-      const uint32_t b = bucket_of(fid[i], F, ltiles);
+      const uint32_t b = bucket_of(fq[r], F, ltiles);
       uint16_t place = kNoSlot;
       if (b < F) {
         place = (uint16_t)atomicAdd(&lcur[b], 1u);
         uint32_t h1, h2;
-        hash16(load_nt(keys + i), h1, h2);
+        hash16(kq[r], h1, h2);
         lhs[place] = make_uint2(h1, h2);
       }
       dest[i] = place;
@@ -583,20 +594,25 @@ __global__ __launch_bounds__(kBlk) void pb_gather_kernel(const uint16_t *__restr
   // it (the last f with lbase[f] <= p, runs of the same filter are
   // contiguous); all kQPT loads of a thread are in flight together
   const uint32_t nvalid = lbase[F];
+  // every gather is issued unconditionally (a place past the block's last
+  // valid one reads that one and is masked), so all kQPT are in flight at once
   uint8_t v[kQPT];
+  uint32_t src[kQPT];
 #pragma unroll
   for (uint32_t r = 0; r < kQPT; ++r) {
-    const uint32_t pl = tid + r * kBlk;
-    v[r] = 0;
-    if (pl < nvalid) {
-      uint32_t lo = 0, hi = F;  // lbase[lo] <= pl < lbase[hi]
-      while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (lbase[mid] <= pl) lo = mid; else hi = mid;
-      }
-      v[r] = res[lstart[lo] + (pl - lbase[lo])];
+    const uint32_t pl = min(tid + r * kBlk, nvalid ? nvalid - 1u : 0u);
+    uint32_t lo = 0, hi = F;  // lbase[lo] <= pl < lbase[hi]
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (lbase[mid] <= pl) lo = mid; else hi = mid;
     }
+    src[r] = lstart[lo] + (pl - lbase[lo]);
   }
+#pragma unroll
+  for (uint32_t r = 0; r < kQPT; ++r) v[r] = nvalid ? res[src[r]] : (uint8_t)0;
+#pragma unroll
+  for (uint32_t r = 0; r < kQPT; ++r)
+    if (tid + r * kBlk >= nvalid) v[r] = 0;
 #pragma unroll
   for (uint32_t r = 0; r < kQPT; ++r) {
     const uint32_t pl = tid + r * kBlk;
