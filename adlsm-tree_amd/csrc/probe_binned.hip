@@ -422,6 +422,7 @@ __global__ __launch_bounds__(kBlk) void pb_bin_kernel(const uint2 *__restrict__ 
 // registers at the tile's start and keeps two runs' loads in flight.
 constexpr uint32_t kTileVecPT = kTileBytes / 16 / kBlk;  // 16-byte tile vectors per thread
 constexpr int kRunLoads = 6;                             // entries per run per stage: 6 x 64 (runs average ~320)
+constexpr uint32_t kZRing = 256;                         // per-wave ring of answers to zero (128 when F > 3071)
 
 struct TileRef {
   uint32_t f, t, sh, nvec, tail;
@@ -461,6 +462,32 @@ __global__ __launch_bounds__(kBlk) void pb_tile_kernel(const uint8_t *__restrict
   uint32_t *ltile = lds;  // the tile's bitmap bytes from a 16-byte-aligned start (+ <= 15 bytes before it)
   uint32_t *ltb = lds + (kTileBytes + 64) / 4;  // the filters' first tiles (F+1), for the tile -> filter search
   const int tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid / kWave;
+  // A clear bit zeroes its query's answer.  Stores count with the run loads
+  // in vmcnt, in issue order, so a store issued between two stages of loads
+  // makes the wait for the later stage wait for the store too.  So each wave
+  // collects the answer indices of its clear bits in a private LDS ring and
+  // stores them after the tile's last run (64 per store instruction); only a
+  // ring that is nearly full flushes earlier.
+  const uint32_t zring = F + 1 <= 3072 ? kZRing : kZRing / 2, zmask = zring - 1;
+  uint32_t *zbuf = lds + (kTileBytes + 64) / 4 + ((F + 1 + 3) & ~3u) + (uint32_t)wave * zring;
+  uint32_t zhead = 0, zcnt = 0;  // wave-uniform
+  auto zflush64 = [&]() {
+    // this wave's LDS writes are done before its reads below (in order)
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    if ((uint32_t)lane < zcnt) res[zbuf[(zhead + lane) & zmask]] = 0;
+    const uint32_t done = zcnt < (uint32_t)kWave ? zcnt : (uint32_t)kWave;
+    zhead = (zhead + done) & zmask;
+    zcnt -= done;
+  };
+  auto zero_answer = [&](bool clr, uint32_t idx) {
+    const uint64_t m = __ballot(clr);
+    if (m == 0) return;
+    const uint32_t before = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    if (clr) zbuf[(zhead + zcnt + before) & zmask] = idx;
+    zcnt += (uint32_t)__popcll(m);
+    if (zcnt > zring - (uint32_t)kWave) zflush64();  // room for the next 64
+  };
   constexpr int NW = kBlk / kWave;
   const uint32_t total_tiles = scal[0];
   for (uint32_t f = tid; f <= F; f += kBlk) ltb[f] = desc[f].tile_base;
@@ -502,8 +529,11 @@ __global__ __launch_bounds__(kBlk) void pb_tile_kernel(const uint8_t *__restrict
     // this wave's runs: chunks wave + NW*q; lane q holds run q's (start, end)
     const uint32_t nq = nc > (uint32_t)wave ? (nc - wave + NW - 1) / NW : 0u;
     __syncthreads();  // the tile is in LDS
-    // two-stage pipeline over the wave's runs: run q+1's first 8 x 64
-    // entries are in flight while run q is tested
+    // Two-stage pipeline over the wave's runs cut into stages of at most
+    // kRunLoads x 64 entries (a long run is several stages): stage s+1's loads
+    // are in flight while stage s is tested.  Every stage issues all its loads
+    // unconditionally -- past the last run an empty stage re-reads a valid
+    // entry -- so the compiler can count them and wait for one stage only.
     struct Stage {
       uint32_t x[kRunLoads];
       uint32_t b0, b1, jc;
@@ -516,58 +546,60 @@ __global__ __launch_bounds__(kBlk) void pb_tile_kernel(const uint8_t *__restrict
 #pragma unroll
       for (int u = 0; u < kRunLoads; ++u) {
         const uint32_t idx = b0 + u * kWave + lane;
-        // an empty run reads entry b0-1: inside the workspace, unused
-        sg.x[u] = (exp & 4) ? (idx * 2654435761u) & 0x7fffffu : run[min(idx, b1 - 1u)];
+        // an empty stage reads entry b0 - 1 (or entry 0): inside the workspace, unused
+        sg.x[u] = (exp & 4) ? (idx * 2654435761u) & 0x7fffffu : run[min(idx, b1 > 0 ? b1 - 1u : 0u)];
       }
     };
-    // 8 entries per lane: all 8 LDS words are read before any is tested (the
-    // reads are unconditional -- a lane past the run holds a clamped entry of
-    // it -- so they issue back to back), then the clear bits store 0
-    auto test8 = [&](const uint32_t (&x)[kRunLoads], uint32_t o, uint32_t b1, uint8_t *rq) {
+    // all kRunLoads LDS words are read before any is tested (the reads are
+    // unconditional -- a lane past the stage holds a clamped entry -- so they
+    // issue back to back), then the clear bits go to the zero ring
+    auto consume = [&](const Stage &sg) {
+      const uint32_t rq = d.qbase + sg.jc * C;  // the chunk's first answer (n < 2^31)
       uint32_t w[kRunLoads];
 #pragma unroll
-      for (int u = 0; u < kRunLoads; ++u) w[u] = ltile[((x[u] & ((1u << kTL) - 1u)) + now.sh) >> 5];
+      for (int u = 0; u < kRunLoads; ++u) w[u] = ltile[((sg.x[u] & ((1u << kTL) - 1u)) + now.sh) >> 5];
 #pragma unroll
       for (int u = 0; u < kRunLoads; ++u) {
-        const uint32_t bit = (x[u] & ((1u << kTL) - 1u)) + now.sh;
-        if (o + u * kWave + lane < b1 && !((w[u] >> (bit & 31)) & 1u) && !(exp & 1)) rq[x[u] >> kTL] = 0;
-      }
-    };
-    auto consume = [&](const Stage &sg) {
-      uint8_t *rq = res + d.qbase + (uint64_t)sg.jc * C;
-      test8(sg.x, sg.b0, sg.b1, rq);
-      // a run longer than 8 x 64 entries (few tiles per filter): the rest
-      const uint32_t *run = ent + (uint64_t)(d.chunk_base + sg.jc) * k * C;
-      for (uint32_t o = sg.b0 + kRunLoads * kWave; o < sg.b1; o += kRunLoads * kWave) {
-        uint32_t x[kRunLoads];
-#pragma unroll
-        for (int u = 0; u < kRunLoads; ++u) x[u] = run[min(o + u * kWave + lane, sg.b1 - 1u)];
-        test8(x, o, sg.b1, rq);
+        const uint32_t bit = (sg.x[u] & ((1u << kTL) - 1u)) + now.sh;
+        const bool clr = sg.b0 + u * kWave + lane < sg.b1 && !((w[u] >> (bit & 31)) & 1u) && !(exp & 1);
+        zero_answer(clr, rq + (sg.x[u] >> kTL));
       }
     };
     for (uint32_t q0 = 0; q0 < nq; q0 += kWave) {
-      uint32_t rs = 0, re = 0;
-      if (q0 + lane < nq) {
-        const uint32_t jc = wave + NW * (q0 + lane);
+      const uint32_t nr = min((uint32_t)kWave, nq - q0);
+      uint32_t rs, re;
+      {
+        const uint32_t jc = wave + NW * (q0 + min((uint32_t)lane, nr - 1u));
         rs = row[jc];
         re = row[nc + jc];
       }
-      const uint32_t nr = min((uint32_t)kWave, nq - q0);
-      Stage A, B;
-      issue(A, __builtin_amdgcn_readlane(rs, 0), __builtin_amdgcn_readlane(re, 0), wave + NW * q0);
-      for (uint32_t q = 0; q < nr; q += 2) {
-        if (q + 1 < nr)
-          issue(B, __builtin_amdgcn_readlane(rs, q + 1), __builtin_amdgcn_readlane(re, q + 1),
-                wave + NW * (q0 + q + 1));
-        consume(A);
-        if (q + 1 < nr) {
-          if (q + 2 < nr)
-            issue(A, __builtin_amdgcn_readlane(rs, q + 2), __builtin_amdgcn_readlane(re, q + 2),
-                  wave + NW * (q0 + q + 2));
-          consume(B);
+      // the stage cursor: run sq of this batch, entries from so
+      uint32_t sq = 0, so = __builtin_amdgcn_readlane(rs, 0);
+      auto take = [&](Stage &sg) {
+        const bool more = sq < nr;  // wave-uniform
+        const uint32_t qe = more ? __builtin_amdgcn_readlane(re, sq) : 0u;
+        const uint32_t b0 = more ? so : 0u;
+        const uint32_t b1 = more ? min(so + (uint32_t)(kRunLoads * kWave), qe) : 0u;
+        const uint32_t jc = wave + NW * (q0 + (more ? sq : nr - 1u));
+        issue(sg, b0, b1, jc);
+        if (more) {
+          so = b1;
+          if (so >= qe) {
+            ++sq;
+            if (sq < nr) so = __builtin_amdgcn_readlane(rs, sq);
+          }
         }
+      };
+      Stage A, B;
+      take(A);
+      while (A.b1 > A.b0) {
+        take(B);
+        consume(A);
+        take(A);
+        consume(B);
       }
     }
+    while (zcnt) zflush64();  // this tile's answers, after its last run
   }
 }
 
@@ -678,7 +710,8 @@ int adl_bloom_probe_batch_device(const uint8_t *d_keys, const uint64_t *d_offset
   const size_t lds_k3 = (size_t)(2 * kQB + 5 * (F + 1) + 32) * 4;      // hashes + 5 per-filter arrays + scratch
   const size_t lds_k6 = (size_t)(kQB / 4 + 3 * (F + 1) + 32) * 4;      // answers + 3 per-filter arrays + scratch
   const size_t lds_p1 = (size_t)(kMaxTiles + 4 + 64 + p.k * p.C) * 4;
-  const size_t lds_p2 = (size_t)kTileBytes + 64 + (size_t)(F + 1) * 4;
+  const size_t lds_p2 = (size_t)kTileBytes + 64 + (size_t)((F + 1 + 3) & ~3u) * 4 +
+                        (size_t)(kBlk / kWave) * (F + 1 <= 3072 ? kZRing : kZRing / 2) * 4;
   try {
     hipLaunchKernelGGL(pb_desc_kernel, dim3(1), dim3(kBlk), 0, st, d_bitmap_off, d_bitmap_end, F, desc, scal);
     ADL_HIP_TRY(hipGetLastError());
