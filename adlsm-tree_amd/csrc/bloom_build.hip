@@ -64,7 +64,8 @@ struct FilterDesc {
   uint32_t chunks;      // W
   uint32_t tiles;       // T
   FastMod mod;          // m = 8 * bitmap bytes
-  uint32_t pad_[2];
+  uint32_t sc_base;     // first hash_var_kernel workgroup (variable-length keys)
+  uint32_t pad_;
 };
 
 struct BuildArgs {
@@ -81,6 +82,8 @@ struct BuildArgs {
   uint32_t stage_keys; // pass A: LDS-staged variable-length keys (16-B aligned key buffer; ADL_BLOOM_STAGE_KEYS)
   uint32_t dedup;      // skip a key equal to its predecessor in the same filter (ADL_BLOOM_SKIP_ADJACENT_DUPLICATES)
   uint32_t scan1;      // pass A: one-barrier tile-count scan (ADL_BLOOM_SCAN1)
+  uint32_t hv_keys;    // keys per hash_var_kernel run (ADL_BLOOM_HV_KEYS)
+  uint32_t var_hash;   // variable-length keys: length-sorted hashing pass + pass A over (h1, h2) (ADL_BLOOM_VAR_HASH)
   uint32_t exp;        // diagnostics build only (ADL_BLOOM_EXP bits, wrong results): pass A 1 no hash,
                        // 2 no position stores; pass B 4 no ds_or, 8 no bitmap stores
   FilterDesc f[kMaxFilters];
@@ -437,6 +440,174 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin_kernel(BuildArgs a, Keys keys
   STAMP_FLUSH(0);
 }
 
+// ---------------------------------------------------------------- var-len hashing
+// Variable-length keys (Zipf lengths) hashed before pass A, in length order.
+// A wave hashes 64 keys in lockstep, so it costs as much as its longest key;
+// keys sorted by exact length within runs of S keys give waves of nearly
+// equal keys.  One workgroup per run of a filter:
+//   sort   key lengths counted into kHvBins exact-length bins in LDS, each
+//          key's (start, length) scattered to its sorted slot;
+//   stage  the run's key bytes copied into LDS with coalesced 16-byte loads
+//          (each byte read from HBM once, in memory order);
+//   hash   wave w takes groups of 64 sorted slots, each lane one key, hashed
+//          from LDS (hash_lds: both seeds, alignbyte words); a key that lies
+//          past the staging buffer is hashed from global memory;
+//   out    (h1, h2) of sorted slot s to hp[chunk_base * C + first + s].
+// The bitmap is an OR over the filter's keys, so pass A may take them in this
+// order.  Pass A then reads 8 bytes per key (bloom_bin16_kernel over SrcH).
+// Workgroups are small (256 threads), two per CU, so one workgroup's sort and
+// staging overlap the other's hashing; no barrier waits for the slowest group
+// (a workgroup ends when its last wave does).
+// Measured against hashing in sorted order straight from global memory (lanes
+// reading scattered keys): L2 missed each key line ~3.7 times, 1.4 GB fetched
+// for 0.4 GB of keys.
+constexpr int kHvBlock = 256;
+constexpr uint32_t kHvBins = 512;          // exact key length 0..510; 511 = longer
+// LDS staging of a run's key bytes: 48 bytes per key (mean key ~40 B)
+template <uint32_t S>
+constexpr uint32_t hv_stage_bytes() {
+  return S * 48;
+}
+
+template <uint32_t S>
+constexpr size_t hv_lds_bytes() {
+  return kHvBins * 4 + S * 4 + S * 2 + hv_stage_bytes<S>() + 16;
+}
+
+template <uint32_t S>
+__global__ __launch_bounds__(kHvBlock) void hash_var_kernel(BuildArgs a, KeysVar keys, uint2 *__restrict__ hp,
+                                                            uint32_t total_sc) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  uint32_t *bins = lds;                                             // kHvBins
+  uint32_t *s_rel = lds + kHvBins;                                  // key start - base16, by sorted slot
+  uint16_t *s_len = reinterpret_cast<uint16_t *>(s_rel + S);        // length (0xffff: >= 64 KiB)
+  uint32_t *stage = reinterpret_cast<uint32_t *>(s_len + S);        // 16-byte aligned (S % 8 == 0)
+  constexpr int KPT = S / kHvBlock;
+  constexpr uint32_t NW = kHvBlock / kWave;
+  const int tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid / kWave;
+  const uint32_t sc = blockIdx.x;
+  if (sc >= total_sc) return;
+  int fi = 0;
+#pragma unroll
+  for (int i = 1; i < kMaxFilters; ++i)
+    if ((uint32_t)i < a.nf && sc >= a.f[i].sc_base) fi = i;
+  const FilterDesc &d = a.f[fi];
+  const uint32_t first = (sc - d.sc_base) * S;
+  const uint32_t cnt = min(S, d.n - first);
+  const uint64_t kb = d.key_begin + first;
+  const uint64_t base16 = keys.offs[kb] & ~15ull;
+  const uint64_t end = keys.offs[kb + cnt];
+  // staged: bytes [base16, base16 + sbytes), whole 16-byte blocks, each
+  // holding at least one byte of the run (so every load is in bounds)
+  constexpr uint32_t kStage = hv_stage_bytes<S>();
+  const uint32_t sbytes = (uint32_t)min((end - base16 + 15) & ~15ull, (uint64_t)kStage);
+
+  // ---- sort the run's keys by length; the offset loads are all issued
+  // before the first is used (clamped index: unconditional, countable waits)
+  for (uint32_t i = tid; i < kHvBins; i += kHvBlock) bins[i] = 0;
+  uint64_t o0[KPT], o1[KPT];
+#pragma unroll
+  for (int i = 0; i < KPT; ++i) {
+    const uint32_t idx = min((uint32_t)(tid + i * kHvBlock), cnt - 1u);
+    o0[i] = keys.offs[kb + idx];
+    o1[i] = keys.offs[kb + idx + 1];
+  }
+  __syncthreads();
+  uint32_t rk[KPT];
+#pragma unroll
+  for (int i = 0; i < KPT; ++i) {
+    rk[i] = ~0u;
+    if (tid + i * kHvBlock < cnt) {
+      const uint32_t c = (uint32_t)min(o1[i] - o0[i], (uint64_t)(kHvBins - 1));
+      rk[i] = (atomicAdd(&bins[c], 1u) << 9) | c;
+    }
+  }
+  // stage the key bytes meanwhile: every load in flight before the first LDS
+  // write (one memory round trip for the whole run)
+  {
+    constexpr int VPT = kStage / 16 / kHvBlock;
+    const uint4 *src = reinterpret_cast<const uint4 *>(keys.keys + base16);
+    uint4 *dst = reinterpret_cast<uint4 *>(stage);
+    const uint32_t nv = sbytes / 16;
+    uint4 v[VPT];
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) v[i] = src[min((uint32_t)(tid + i * kHvBlock), nv - 1u)];
+#pragma unroll
+    for (int i = 0; i < VPT; ++i)
+      if (tid + i * kHvBlock < nv) dst[tid + i * kHvBlock] = v[i];
+  }
+  __syncthreads();
+  if (wave == 0) {  // exclusive scan of the bins, 8 per lane
+    constexpr int PER = kHvBins / kWave;
+    uint32_t v[PER], t = 0;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) v[j] = bins[lane * PER + j], t += v[j];
+    uint32_t run = wave_incl_scan(t, lane) - t;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) bins[lane * PER + j] = run, run += v[j];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < KPT; ++i) {
+    if (rk[i] != ~0u) {
+      const uint32_t slot = bins[rk[i] & (kHvBins - 1)] + (rk[i] >> 9);
+      const uint64_t len = o1[i] - o0[i];
+      // a key of 64 KiB or more keeps its index in the run instead of its start
+      s_rel[slot] = len < 0xffffu ? (uint32_t)(o0[i] - base16) : tid + i * kHvBlock;
+      s_len[slot] = (uint16_t)min(len, (uint64_t)0xffffu);
+    }
+  }
+  __syncthreads();
+
+  // ---- hash, group g = 64 sorted slots
+  const uint32_t groups = (cnt + kWave - 1) / kWave;
+  uint2 *out = hp + (uint64_t)d.chunk_base * a.C + first;
+  for (uint32_t g = wave; g < groups; g += NW) {
+    const uint32_t s = g * kWave + lane;
+    if (s >= cnt) break;
+    uint32_t len = s_len[s];
+    const uint32_t r = s_rel[s];
+    uint32_t h1, h2;
+    if (len < 0xffffu && (uint64_t)r + len <= sbytes) {
+      hash_lds(stage, r, len, h1, h2);
+    } else {
+      uint64_t k0 = base16 + r;
+      if (len == 0xffffu) {
+        k0 = keys.offs[kb + r];
+        len = (uint32_t)(keys.offs[kb + r + 1] - k0);
+      }
+      hash_bytes(keys.keys + k0, len, kSeed1, kSeed2, h1, h2);
+    }
+    out[s] = make_uint2(h1, h2);
+  }
+}
+
+// Key sources of bloom_bin16_kernel: raw 16-byte keys (hashed in pass A), or
+// the (h1, h2) pairs hash_var_kernel wrote in pass A's chunk grid.
+struct Src16 {
+  const uint4 *keys;
+  using Raw = uint4;
+  __device__ __forceinline__ Raw load(const FilterDesc &d, uint32_t chunk, uint32_t first, uint32_t idx) const {
+    return load_nt(keys + d.key_begin + first + idx);
+  }
+  __device__ static __forceinline__ void hash(const Raw &r, uint32_t &h1, uint32_t &h2) { hash16(r, h1, h2); }
+};
+
+typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
+struct SrcH {
+  const uint2 *h;
+  uint32_t C;
+  using Raw = uint2;
+  __device__ __forceinline__ Raw load(const FilterDesc &, uint32_t chunk, uint32_t, uint32_t idx) const {
+    const u32x2_t v = __builtin_nontemporal_load(reinterpret_cast<const u32x2_t *>(h + (uint64_t)chunk * C + idx));
+    return make_uint2(v.x, v.y);
+  }
+  __device__ static __forceinline__ void hash(const Raw &r, uint32_t &h1, uint32_t &h2) {
+    h1 = r.x;
+    h2 = r.y;
+  }
+};
+
 // Pass A for the hot path (16-byte keys, compile-time k).  Same output as
 // bloom_bin_kernel, with the chunk loop software-pipelined so VALU, LDS and
 // memory overlap inside one workgroup:
@@ -446,8 +617,8 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin_kernel(BuildArgs a, Keys keys
 //   prefetch keys of c+2
 // so the murmur work hides under the scatter's LDS latency and the position
 // stores drain under the next count.
-template <int BLOCK, int K>
-__global__ __launch_bounds__(BLOCK) void bloom_bin16_kernel(BuildArgs a, Keys16 keys,
+template <int BLOCK, int K, class Src>
+__global__ __launch_bounds__(BLOCK) void bloom_bin16_kernel(BuildArgs a, Src keys,
                                                               uint32_t *__restrict__ pos_ws,
                                                               uint32_t *__restrict__ table_ws,
                                                               uint32_t total_chunks, uint32_t *__restrict__ tile_queue) {
@@ -479,26 +650,27 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin16_kernel(BuildArgs a, Keys16 
   uint4 *dummy4 = reinterpret_cast<uint4 *>(dummy);
   constexpr int TPT = (int)((kHistMax + BLOCK - 1) / BLOCK);  // table entries per thread, at most
 
-  auto fetch = [&](uint32_t chunk, uint4 (&raw)[KPT]) {
+  using Raw = typename Src::Raw;
+  auto fetch = [&](uint32_t chunk, Raw (&raw)[KPT]) {
     const FilterDesc &d = a.f[find_filter_by_chunk(a, chunk)];
     const uint32_t first = (chunk - d.chunk_base) * C;
     const uint32_t last = min(C, d.n - first) - 1u;
 #pragma unroll
     for (int i = 0; i < KPT; ++i) {
       const uint32_t idx = min((uint32_t)(tid + i * BLOCK), last);
-      raw[i] = load_nt(keys.keys + d.key_begin + first + idx);
+      raw[i] = keys.load(d, chunk, first, idx);
     }
   };
 
   // The keys of chunk c+2 load at the end of step c (two chunks ahead) and
   // are hashed in step c+1.  Measured against loading chunk c+1's keys at the
   // top of step c (no load in flight across the back-edge): 111 vs 127 us.
-  uint4 raw[KPT];
+  Raw raw[KPT];
   uint32_t h1[KPT], h2[KPT];
   if (slot >= total_chunks) return;
   fetch(slot, raw);
 #pragma unroll
-  for (int i = 0; i < KPT; ++i) hash16(raw[i], h1[i], h2[i]);
+  for (int i = 0; i < KPT; ++i) Src::hash(raw[i], h1[i], h2[i]);
   fetch(min(slot + G, total_chunks - 1), raw);
   for (uint32_t i = tid; i < a.hist_words; i += BLOCK) hist[i] = 0;
 
@@ -572,7 +744,7 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin16_kernel(BuildArgs a, Keys16 
         h2[i] = raw[i].y | 1u;
       } else
 #endif
-      hash16(raw[i], h1[i], h2[i]);
+      Src::hash(raw[i], h1[i], h2[i]);
     }
     fetch(min(wg + 2 * G, total_chunks - 1), raw);
     __syncthreads();  // lpos holds chunk c sorted; hist is free
@@ -830,8 +1002,8 @@ inline KeysVar shift_keys(KeysVar k, uint64_t b) { k.offs += b; return k; }
 // ---------------------------------------------------------------- host plan
 struct Plan {
   BuildArgs a;
-  uint64_t pos_words = 0, table_words = 0, scratch_words = 0, ws_bytes = 0;
-  uint32_t total_chunks = 0, total_tiles = 0;
+  uint64_t pos_words = 0, table_words = 0, scratch_words = 0, hash_words = 0, ws_bytes = 0;
+  uint32_t total_chunks = 0, total_tiles = 0, total_sc = 0;
   uint32_t grid_a = 0, grid_b = 0;  // persistent grids
   uint32_t block_a = 512;             // pass A threads per workgroup
   uint32_t depth = kDepthB;           // pass B descriptors per step
@@ -914,6 +1086,11 @@ int make_plan(const uint64_t *counts, uint32_t nf, int32_t bpk, Plan &p) {
   p.a.dyn_tiles = env_flag("ADL_BLOOM_DYN_TILES", 0);
   p.a.stage_keys = env_flag("ADL_BLOOM_STAGE_KEYS", 1);
   p.a.scan1 = env_flag("ADL_BLOOM_SCAN1", 1);
+  p.a.var_hash = env_flag("ADL_BLOOM_VAR_HASH", 1);
+  {
+    const uint32_t hk = env_u32("ADL_BLOOM_HV_KEYS", 512);
+    p.a.hv_keys = hk <= 256 ? 256 : hk <= 512 ? 512 : hk <= 1024 ? 1024 : 2048;
+  }
 #ifdef ADL_BLOOM_STAMPS
   p.a.exp = env_u32("ADL_BLOOM_EXP", 0);  // diagnostics build only
 #else
@@ -926,7 +1103,7 @@ int make_plan(const uint64_t *counts, uint32_t nf, int32_t bpk, Plan &p) {
   p.a.cap = cap;
   p.a.hist_words = hist_words;
   uint64_t pos = 0, tab = 0, boff = 0;
-  uint32_t chunk = 0, tile = 0;
+  uint32_t chunk = 0, tile = 0, sc = 0;
   for (uint32_t f = 0; f < nf; ++f) {
     FilterDesc &d = p.a.f[f];
     const uint64_t bytes = adl_host::bitmap_bytes(counts[f], bpk);
@@ -939,6 +1116,8 @@ int make_plan(const uint64_t *counts, uint32_t nf, int32_t bpk, Plan &p) {
     d.mod = adl_host::make_fastmod(m);
     d.chunk_base = chunk;
     d.tile_base = tile;
+    d.sc_base = sc;
+    sc += (uint32_t)((counts[f] + p.a.hv_keys - 1) / p.a.hv_keys);
     d.pos_base = pos;
     d.table_base = tab;
     d.bitmap_off = boff;  // overwritten by the caller
@@ -951,12 +1130,17 @@ int make_plan(const uint64_t *counts, uint32_t nf, int32_t bpk, Plan &p) {
   if (pos + 64 >= (1ull << 32)) return ADL_ERR_TOO_LARGE;  // u32 position indices
   p.total_chunks = chunk;
   p.total_tiles = tile;
+  p.total_sc = sc;
   p.pos_words = adl_host::round_up(pos, 64);
   p.table_words = adl_host::round_up(tab + kTablePad, 64);
   // after the table: pass B's tile queue (64 words), then one 16-byte scratch
   // line per pass-A wave (bloom_bin16_kernel's masked-off stores)
   p.scratch_words = 64 + (uint64_t)grid_a_max * (block_a / kWave) * 4;
-  p.ws_bytes = (p.pos_words + p.table_words + p.scratch_words) * 4 + 256;
+  // then (h1, h2) per key in the chunk grid: hash_var_kernel -> pass A
+  // (variable-length keys; reserved for every key shape so the workspace size
+  // does not depend on it)
+  p.hash_words = adl_host::round_up(2ull * chunk * C, 64);
+  p.ws_bytes = (p.pos_words + p.table_words + p.scratch_words + p.hash_words) * 4 + 256;
   p.lds_a = (size_t)(hist_words + 32 + (k + 1) * C + 256) * 4;
   p.lds_b = (size_t)((1u << (TL - 5)) + 2 * kSegBatch + 4) * 4;
   p.grid_a = std::min<uint32_t>(p.total_chunks, grid_a_max);
@@ -1004,18 +1188,42 @@ int launch_binned(const Plan &p, Keys keys, uint8_t *d_bitmaps, void *ws, hipStr
     ADL_HIP_TRY(hipEventRecord(ev[1], st));
   }
   if (p.total_chunks) {
-    auto go = [&](auto kern) -> int {
+    uint2 *hp = reinterpret_cast<uint2 *>(queue + p.scratch_words);
+    auto go_src = [&](auto kern, auto src, bool hashed) -> int {
       ADL_HIP_TRY(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                                       (int)p.lds_a));
-      hipExtLaunchKernelGGL(kern, dim3(p.grid_a), dim3(p.block_a), p.lds_a, st, ev ? ev[0] : nullptr,
-                            ev ? ev[1] : nullptr, 0, p.a, keys, pos_ws, tab_ws, p.total_chunks, queue);
+      hipExtLaunchKernelGGL(kern, dim3(p.grid_a), dim3(p.block_a), p.lds_a, st,
+                            ev && !hashed ? ev[0] : nullptr, ev ? ev[1] : nullptr, 0, p.a, src, pos_ws, tab_ws,
+                            p.total_chunks, queue);
       ADL_HIP_TRY(hipGetLastError());
       return ADL_OK;
     };
+    auto go = [&](auto kern) -> int { return go_src(kern, keys, false); };
     auto by_block = [&](auto k6, auto kgen) -> int {  // k6/kgen: tag types carrying BLOCK
       constexpr int B = decltype(k6)::value;
       if constexpr (std::is_same<Keys, Keys16>::value) {
-        if (p.a.k == 6 && !p.sequential_a && !p.a.dedup) return go(bloom_bin16_kernel<B, 6>);
+        if (p.a.k == 6 && !p.sequential_a && !p.a.dedup)
+          return go_src(bloom_bin16_kernel<B, 6, Src16>, Src16{keys.keys}, false);
+      }
+      if constexpr (std::is_same<Keys, KeysVar>::value) {
+        // length-sorted hashing pass, then pass A over the (h1, h2) pairs; the
+        // profiled pass-A interval spans both launches
+        if (p.a.k == 6 && p.a.var_hash && !p.sequential_a && !p.a.dedup) {
+          auto hv_go = [&](auto kern, size_t lds) -> int {
+            ADL_HIP_TRY(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                            (int)lds));
+            hipExtLaunchKernelGGL(kern, dim3(p.total_sc), dim3(kHvBlock), lds, st, ev ? ev[0] : nullptr, nullptr, 0,
+                                  p.a, keys, hp, p.total_sc);
+            ADL_HIP_TRY(hipGetLastError());
+            return ADL_OK;
+          };
+          const int rh = p.a.hv_keys == 256    ? hv_go(hash_var_kernel<256>, hv_lds_bytes<256>())
+                         : p.a.hv_keys == 512  ? hv_go(hash_var_kernel<512>, hv_lds_bytes<512>())
+                         : p.a.hv_keys == 1024 ? hv_go(hash_var_kernel<1024>, hv_lds_bytes<1024>())
+                                               : hv_go(hash_var_kernel<2048>, hv_lds_bytes<2048>());
+          if (rh) return rh;
+          return go_src(bloom_bin16_kernel<B, 6, SrcH>, SrcH{hp, p.a.C}, true);
+        }
       }
       if (p.a.k == 6) return go(bloom_bin_kernel<B, 6, 6, Keys>);
       return go(bloom_bin_kernel<B, 0, kKptMax, Keys>);

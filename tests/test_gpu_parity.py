@@ -187,6 +187,44 @@ def test_build_synth_zipf_varlen(dev, ab, oracle):
     assert np.array_equal(bm, oracle.keys2block(data.cpu().numpy(), h_off))
 
 
+def test_build_varlen_long_and_mixed_keys(dev, ab, oracle):
+    # the length-sorted hashing pass: keys of 0..3000 bytes (several load windows
+    # per key, the longer-than-510 bin), a run of 70 equal 511-byte keys, bytes
+    # >= 0x80, and a buffer that ends exactly at the last key (its lanes hash
+    # bytewise instead of reading past the end)
+    rng = random.Random(31)
+    keys = [rng.randbytes(rng.randrange(0, 3001)) for _ in range(3000)]
+    keys += [b"x" * 511] * 70 + [bytes([0x80 + i % 100]) * (i % 41) for i in range(200)]
+    rng.shuffle(keys)
+    data, offs = oracle.pack(keys)
+    data = data[: int(offs[-1])]
+    bm = ab.build(to_dev(dev, data), to_dev(dev, offs.view(np.int64))).cpu().numpy()
+    assert np.array_equal(bm, oracle.keys2block(data, offs))
+
+
+@pytest.mark.parametrize("var_hash", ["0", "1"])
+def test_build_varlen_hash_pass_switch(dev, ab, oracle, monkeypatch, var_hash):
+    # ADL_BLOOM_VAR_HASH=0 is the fused pass A that hashes inside the chunk loop
+    monkeypatch.setenv("ADL_BLOOM_VAR_HASH", var_hash)
+    data, offs = ab.synth_varlen(120_000, seed=77)
+    bm = ab.build(data, offs).cpu().numpy()
+    assert np.array_equal(bm, oracle.keys2block(data.cpu().numpy(), offs.cpu().numpy().view(np.uint64)))
+
+
+def test_build_segmented_varlen_superchunk_edges(dev, ab, oracle):
+    # filters of 4096-key hashing runs +-1, empty and 1-key filters in one launch
+    rng = random.Random(12)
+    sizes = [4095, 4096, 4097, 1, 0, 8193, 2, 12000]
+    kb = np.concatenate([[0], np.cumsum(sizes)]).astype(np.uint64)
+    keys = [rng.randbytes(rng.randrange(0, 90)) for _ in range(int(kb[-1]))]
+    dk, do, data, offs = packed_dev(dev, keys)
+    out, boff, nbytes = ab.build_segmented(dk, kb, offsets=do)
+    out = out.cpu().numpy()
+    for f in range(len(sizes)):
+        got = out[int(boff[f]):int(boff[f]) + int(nbytes[f])]
+        assert np.array_equal(got, oracle.keys2block(keys[int(kb[f]):int(kb[f + 1])])), f
+
+
 @pytest.mark.parametrize("stride", [1, 4, 7, 9, 24, 32])
 def test_build_fixed_stride(dev, ab, oracle, stride):
     rng = np.random.default_rng(stride)

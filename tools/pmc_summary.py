@@ -12,10 +12,11 @@ acc = defaultdict(lambda: defaultdict(list))
 for f in sorted(glob.glob(os.path.join(root, "p*", "**", "*counter_collection.csv"), recursive=True)):
     for row in csv.DictReader(open(f)):
         k = row.get("Kernel_Name", "?")
-        short = "bin" if "bloom_bin" in k else "tile" if "bloom_tile" in k else k[:40]
+        short = ("bin" if "bloom_bin" in k else "tile" if "bloom_tile" in k else "hash_var" if "hash_var" in k
+                 else k[:40])
         acc[short][row["Counter_Name"]].append(float(row["Counter_Value"]))
 for k, cs in acc.items():
-    if k not in ("bin", "tile"):
+    if k not in ("bin", "tile", "hash_var"):
         continue
     print(f"== {k}")
     for c, v in sorted(cs.items()):
