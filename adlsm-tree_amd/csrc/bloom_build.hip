@@ -502,8 +502,11 @@ __global__ __launch_bounds__(kHvBlock) void hash_var_kernel(BuildArgs a, KeysVar
   constexpr uint32_t kStage = hv_stage_bytes<S>();
   const uint32_t sbytes = (uint32_t)min((end - base16 + 15) & ~15ull, (uint64_t)kStage);
 
-  // ---- sort the run's keys by length; the offset loads are all issued
-  // before the first is used (clamped index: unconditional, countable waits)
+  // ---- load the run's offsets and key bytes: every load in flight before
+  // the first is used (clamped indices: unconditional, countable waits), so
+  // the run costs one memory round trip
+  constexpr int VPT = kStage / 16 / kHvBlock;
+  const uint32_t nv = sbytes / 16;
   for (uint32_t i = tid; i < kHvBins; i += kHvBlock) bins[i] = 0;
   uint64_t o0[KPT], o1[KPT];
 #pragma unroll
@@ -512,7 +515,14 @@ __global__ __launch_bounds__(kHvBlock) void hash_var_kernel(BuildArgs a, KeysVar
     o0[i] = keys.offs[kb + idx];
     o1[i] = keys.offs[kb + idx + 1];
   }
+  u32x4_t v[VPT];  // (the ext-vector type: an array of uint4 held across the barrier goes to scratch)
+  {
+    const u32x4_t *src = reinterpret_cast<const u32x4_t *>(keys.keys + base16);
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) v[i] = src[min((uint32_t)(tid + i * kHvBlock), nv - 1u)];
+  }
   __syncthreads();
+  // ---- sort the run's keys by length
   uint32_t rk[KPT];
 #pragma unroll
   for (int i = 0; i < KPT; ++i) {
@@ -522,16 +532,8 @@ __global__ __launch_bounds__(kHvBlock) void hash_var_kernel(BuildArgs a, KeysVar
       rk[i] = (atomicAdd(&bins[c], 1u) << 9) | c;
     }
   }
-  // stage the key bytes meanwhile: every load in flight before the first LDS
-  // write (one memory round trip for the whole run)
   {
-    constexpr int VPT = kStage / 16 / kHvBlock;
-    const uint4 *src = reinterpret_cast<const uint4 *>(keys.keys + base16);
-    uint4 *dst = reinterpret_cast<uint4 *>(stage);
-    const uint32_t nv = sbytes / 16;
-    uint4 v[VPT];
-#pragma unroll
-    for (int i = 0; i < VPT; ++i) v[i] = src[min((uint32_t)(tid + i * kHvBlock), nv - 1u)];
+    u32x4_t *dst = reinterpret_cast<u32x4_t *>(stage);
 #pragma unroll
     for (int i = 0; i < VPT; ++i)
       if (tid + i * kHvBlock < nv) dst[tid + i * kHvBlock] = v[i];
@@ -539,12 +541,12 @@ __global__ __launch_bounds__(kHvBlock) void hash_var_kernel(BuildArgs a, KeysVar
   __syncthreads();
   if (wave == 0) {  // exclusive scan of the bins, 8 per lane
     constexpr int PER = kHvBins / kWave;
-    uint32_t v[PER], t = 0;
+    uint32_t bv[PER], t = 0;
 #pragma unroll
-    for (int j = 0; j < PER; ++j) v[j] = bins[lane * PER + j], t += v[j];
+    for (int j = 0; j < PER; ++j) bv[j] = bins[lane * PER + j], t += bv[j];
     uint32_t run = wave_incl_scan(t, lane) - t;
 #pragma unroll
-    for (int j = 0; j < PER; ++j) bins[lane * PER + j] = run, run += v[j];
+    for (int j = 0; j < PER; ++j) bins[lane * PER + j] = run, run += bv[j];
   }
   __syncthreads();
 #pragma unroll
