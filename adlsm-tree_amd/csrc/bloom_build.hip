@@ -83,6 +83,8 @@ struct BuildArgs {
   uint32_t dedup;      // skip a key equal to its predecessor in the same filter (ADL_BLOOM_SKIP_ADJACENT_DUPLICATES)
   uint32_t scan1;      // pass A: one-barrier tile-count scan (ADL_BLOOM_SCAN1)
   uint32_t hv_keys;    // keys per hash_var_kernel run (ADL_BLOOM_HV_KEYS)
+  uint32_t dd_log2;    // bloom_bin16_kernel: log2 slots of the (h1, h2) table that skips repeated hashes
+                       // (0: off; ADL_BLOOM_HASH_DEDUP)
   uint32_t var_hash;   // variable-length keys: length-sorted hashing pass + pass A over (h1, h2) (ADL_BLOOM_VAR_HASH)
   uint32_t exp;        // diagnostics build only (ADL_BLOOM_EXP bits, wrong results): pass A 1 no hash,
                        // 2 no position stores; pass B 4 no ds_or, 8 no bitmap stores
@@ -676,11 +678,25 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin16_kernel(BuildArgs a, Src key
   fetch(min(slot + G, total_chunks - 1), raw);
   for (uint32_t i = tid; i < a.hist_words; i += BLOCK) hist[i] = 0;
 
+  // Repeated hashes.  The reference's murmur variant collapses: rotations with
+  // an arithmetic shift and sign-extended bytes leave SplitMix keys only ~69 %
+  // distinct (h1, h2) pairs at 10M keys, one pair 14 723 times.  A key whose
+  // pair another key of this workgroup (same filter) already counted sets no
+  // new bit, so it is skipped.  dtab: 2^dd_log2 slots, claimed with a 64-bit
+  // compare-and-swap (EMPTY -> pair): a key is skipped only when its slot
+  // holds exactly its own pair, installed by a key that was counted.
+  const uint32_t dd = a.dd_log2;
+  unsigned long long *dtab = reinterpret_cast<unsigned long long *>(lpos + K * C);
+  constexpr unsigned long long kEmpty = ~0ull;
+  if (dd)
+    for (uint32_t i = tid; i < (1u << dd); i += BLOCK) dtab[i] = kEmpty;
+
   uint4 *pdst = dummy4;  // deferred store of the previous chunk
   uint32_t ptotal = 0;
   STAMP_DECL
   for (uint32_t wg = slot; wg < total_chunks; wg += G) {
-    const FilterDesc &d = a.f[find_filter_by_chunk(a, wg)];
+    const int fcur = find_filter_by_chunk(a, wg);
+    const FilterDesc &d = a.f[fcur];
     const uint32_t w = wg - d.chunk_base;
     const uint32_t cnt = min(C, d.n - w * C);
     const uint32_t T = d.tiles;
@@ -690,10 +706,28 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin16_kernel(BuildArgs a, Src key
 
     // count(c) + store(c-1)
     const uint32_t pvec = ptotal >> 2;
+    uint32_t live = 0;  // bit i: key slot i is counted
+#pragma unroll
+    for (int i = 0; i < KPT; ++i)
+      if (tid + i * BLOCK < cnt) live |= 1u << i;
+    if (dd) {
+      unsigned long long old[KPT];
+#pragma unroll
+      for (int i = 0; i < KPT; ++i) {
+        const unsigned long long hv = ((unsigned long long)h2[i] << 32) | h1[i];
+        const uint32_t sl = (h1[i] + __builtin_amdgcn_alignbit(h2[i], h2[i], 16)) >> (32 - dd);
+        old[i] = (live >> i) & 1u ? atomicCAS(&dtab[sl], kEmpty, hv) : kEmpty;
+      }
+#pragma unroll
+      for (int i = 0; i < KPT; ++i) {
+        const unsigned long long hv = ((unsigned long long)h2[i] << 32) | h1[i];
+        if (old[i] != kEmpty && old[i] == hv) live &= ~(1u << i);
+      }
+    }
     uint32_t pos[KPT][K];
 #pragma unroll
     for (int i = 0; i < KPT; ++i) {
-      if (tid + i * BLOCK < cnt) {
+      if ((live >> i) & 1u) {
 #pragma unroll
         for (int j = 0; j < K; ++j) pos[i][j] = fastmod(h1[i] + (uint32_t)j * h2[i], mod);
 #pragma unroll
@@ -716,8 +750,8 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin16_kernel(BuildArgs a, Src key
     __syncthreads();  // counts complete; the previous chunk's LDS copy is read out
     STAMP(1);
 
-    if (a.scan1) block_excl_scan_array_1b<BLOCK>(hist, T + 1, scratch);
-    else block_excl_scan_array<BLOCK>(hist, T + 1, scratch);
+    const uint32_t total = a.scan1 ? block_excl_scan_array_1b<BLOCK>(hist, T + 1, scratch)
+                                   : block_excl_scan_array<BLOCK>(hist, T + 1, scratch);
     STAMP(2);
     uint32_t *tab = table_ws + d.table_base;
 #pragma unroll
@@ -733,7 +767,7 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin16_kernel(BuildArgs a, Src key
     // lanes past the end hash a clamped key and never use the result)
 #pragma unroll
     for (int i = 0; i < KPT; ++i) {
-      if (tid + i * BLOCK < cnt) {
+      if ((live >> i) & 1u) {
         uint32_t sl[K];
 #pragma unroll
         for (int j = 0; j < K; ++j) sl[j] = atomicAdd(&hist[pos[i][j] >> TL], 1u);
@@ -752,8 +786,11 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin16_kernel(BuildArgs a, Src key
     __syncthreads();  // lpos holds chunk c sorted; hist is free
     STAMP(4);
     for (uint32_t i = tid; i <= T; i += BLOCK) hist[i] = 0;
+    // the pair table holds one filter's pairs (positions depend on m)
+    if (dd && wg + G < total_chunks && find_filter_by_chunk(a, wg + G) != fcur)
+      for (uint32_t i = tid; i < (1u << dd); i += BLOCK) dtab[i] = kEmpty;
     pdst = reinterpret_cast<uint4 *>(pos_ws + d.pos_base + (uint64_t)w * a.cap);
-    ptotal = K * cnt;
+    ptotal = total;
   }
   // epilogue: the last chunk's store
   const uint32_t pvec = ptotal >> 2;
@@ -1090,6 +1127,14 @@ int make_plan(const uint64_t *counts, uint32_t nf, int32_t bpk, Plan &p) {
   p.a.scan1 = env_flag("ADL_BLOOM_SCAN1", 1);
   p.a.var_hash = env_flag("ADL_BLOOM_VAR_HASH", 1);
   {
+    // pair table in the C + 256 words pass A reserves past the positions
+    // (the var-len length sort's area; bloom_bin16_kernel does not use it)
+    const uint32_t lg_max = std::min<uint32_t>(env_u32("ADL_BLOOM_DD_LOG2", 11), 12);
+    uint32_t lg = 0;
+    while (lg < lg_max && (2u << (lg + 1)) <= C + 256) ++lg;
+    p.a.dd_log2 = (env_flag("ADL_BLOOM_HASH_DEDUP", 1) && lg >= 4) ? lg : 0;
+  }
+  {
     const uint32_t hk = env_u32("ADL_BLOOM_HV_KEYS", 512);
     p.a.hv_keys = hk <= 256 ? 256 : hk <= 512 ? 512 : hk <= 1024 ? 1024 : 2048;
   }
@@ -1224,7 +1269,16 @@ int launch_binned(const Plan &p, Keys keys, uint8_t *d_bitmaps, void *ws, hipStr
                          : p.a.hv_keys == 1024 ? hv_go(hash_var_kernel<1024>, hv_lds_bytes<1024>())
                                                : hv_go(hash_var_kernel<2048>, hv_lds_bytes<2048>());
           if (rh) return rh;
-          return go_src(bloom_bin16_kernel<B, 6, SrcH>, SrcH{hp, p.a.C}, true);
+          // the pair table pays for 16-byte keys only (configs[2]'s keys repeat few pairs:
+          // pass B 64 -> 70 us with it)
+          BuildArgs av = p.a;
+          av.dd_log2 = 0;
+          ADL_HIP_TRY(hipFuncSetAttribute((const void *)bloom_bin16_kernel<B, 6, SrcH>,
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)p.lds_a));
+          hipExtLaunchKernelGGL(bloom_bin16_kernel<B, 6, SrcH>, dim3(p.grid_a), dim3(p.block_a), p.lds_a, st, nullptr,
+                                ev ? ev[1] : nullptr, 0, av, SrcH{hp, p.a.C}, pos_ws, tab_ws, p.total_chunks, queue);
+          ADL_HIP_TRY(hipGetLastError());
+          return ADL_OK;
         }
       }
       if (p.a.k == 6) return go(bloom_bin_kernel<B, 6, 6, Keys>);
