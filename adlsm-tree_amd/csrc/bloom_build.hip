@@ -85,6 +85,7 @@ struct BuildArgs {
   uint32_t hv_keys;    // keys per hash_var_kernel run (ADL_BLOOM_HV_KEYS)
   uint32_t dd_log2;    // bloom_bin16_kernel: log2 slots of the (h1, h2) table that skips repeated hashes
                        // (0: off; ADL_BLOOM_HASH_DEDUP)
+  uint32_t dd_mode;    // 1: every key claims its (h1, h2); 2: keys with h1 == h2 claim h1 (ADL_BLOOM_DD_MODE)
   uint32_t var_hash;   // variable-length keys: length-sorted hashing pass + pass A over (h1, h2) (ADL_BLOOM_VAR_HASH)
   uint32_t exp;        // diagnostics build only (ADL_BLOOM_EXP bits, wrong results): pass A 1 no hash,
                        // 2 no position stores; pass B 4 no ds_or, 8 no bitmap stores
@@ -685,8 +686,12 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin16_kernel(BuildArgs a, Src key
   // new bit, so it is skipped.  dtab: 2^dd_log2 slots, claimed with a 64-bit
   // compare-and-swap (EMPTY -> pair): a key is skipped only when its slot
   // holds exactly its own pair, installed by a key that was counted.
-  const uint32_t dd = a.dd_log2;
+  // dd_mode 2: only keys whose seeds converged (h1 == h2: 39 % of the keys,
+  // 90 % of the repeats) claim, a 32-bit CAS of h1 into a table of twice the
+  // slots.
+  const uint32_t dd = a.dd_log2, dd2 = a.dd_mode == 2;
   unsigned long long *dtab = reinterpret_cast<unsigned long long *>(lpos + K * C);
+  uint32_t *dtab32 = lpos + K * C;
   constexpr unsigned long long kEmpty = ~0ull;
   if (dd)
     for (uint32_t i = tid; i < (1u << dd); i += BLOCK) dtab[i] = kEmpty;
@@ -710,7 +715,17 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin16_kernel(BuildArgs a, Src key
 #pragma unroll
     for (int i = 0; i < KPT; ++i)
       if (tid + i * BLOCK < cnt) live |= 1u << i;
-    if (dd) {
+    if (dd && dd2) {
+      uint32_t old[KPT];
+#pragma unroll
+      for (int i = 0; i < KPT; ++i) {
+        const uint32_t sl = h1[i] >> (31 - dd);
+        old[i] = ((live >> i) & 1u) && h1[i] == h2[i] ? atomicCAS(&dtab32[sl], ~0u, h1[i]) : ~0u;
+      }
+#pragma unroll
+      for (int i = 0; i < KPT; ++i)
+        if (old[i] != ~0u && old[i] == h1[i] && h1[i] == h2[i]) live &= ~(1u << i);
+    } else if (dd) {
       unsigned long long old[KPT];
 #pragma unroll
       for (int i = 0; i < KPT; ++i) {
@@ -1133,6 +1148,7 @@ int make_plan(const uint64_t *counts, uint32_t nf, int32_t bpk, Plan &p) {
     uint32_t lg = 0;
     while (lg < lg_max && (2u << (lg + 1)) <= C + 256) ++lg;
     p.a.dd_log2 = (env_flag("ADL_BLOOM_HASH_DEDUP", 1) && lg >= 4) ? lg : 0;
+    p.a.dd_mode = env_u32("ADL_BLOOM_DD_MODE", 2) == 1 ? 1 : 2;
   }
   {
     const uint32_t hk = env_u32("ADL_BLOOM_HV_KEYS", 512);

@@ -12,11 +12,12 @@ if [ -n "${TESTS:-}" ]; then
     > "$OUT/pytest.log" 2>&1; rc=$?; echo "pytest: $(tail -n 1 $OUT/pytest.log)"; [ $rc -ne 0 ] && exit $rc
 fi
 for v in ${VALS:-0 1 0 1}; do
+  tag=$(basename "$(dirname "$v")")_$(basename "$v")
   for wl in $WL; do
     env $KNOB=$v timeout -k 10 300 python3 bench.py --steps 20 --warmup 3 --workload $wl --no-cpu-baseline --no-e2e \
-      > "$OUT/bench_${wl}_$v.log" 2>&1 || exit 1
+      > "$OUT/bench_${wl}_$tag.log" 2>&1 || exit 1
     echo -n "$wl $KNOB=$v: "
-    grep '^{' "$OUT/bench_${wl}_$v.log" | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"], d["roofline"]["us_per_step"], d["parity"])'
+    grep '^{' "$OUT/bench_${wl}_$tag.log" | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"], d["roofline"]["us_per_step"], d["parity"])'
   done
 done
 exit 0
