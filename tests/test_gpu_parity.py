@@ -258,6 +258,26 @@ def test_build_segmented_vs_oracle(dev, ab, oracle):
         assert np.array_equal(got, want), f
 
 
+@pytest.mark.parametrize("dedup", ["0", "1"])
+def test_build_segmented_same_keys_every_filter(dev, ab, oracle, monkeypatch, dedup):
+    # pass A skips a key whose hash pair its workgroup already counted; the pair
+    # table must start over at a filter boundary (positions depend on m), so
+    # filters holding the same keys each get every bit.  4 x 500k keys = 360
+    # chunks > one grid round, so workgroups cross filters.
+    monkeypatch.setenv("ADL_BLOOM_HASH_DEDUP", dedup)
+    n = 500_000
+    base = ab.synth_keys16(n, seed=0xD0D0)
+    keys = dev.cat([base, base, base[: n // 2], base])
+    sizes = [n, n, n // 2, n]
+    kb = np.concatenate([[0], np.cumsum(sizes)]).astype(np.uint64)
+    out, boff, nbytes = ab.build_segmented(keys, kb)
+    out = out.cpu().numpy()
+    hk = base.cpu().numpy()
+    for f, m in enumerate(sizes):
+        got = out[int(boff[f]):int(boff[f]) + int(nbytes[f])]
+        assert np.array_equal(got, oracle.keys2block(hk[:m])), f
+
+
 def test_build_segmented_varlen(dev, ab, oracle):
     rng = random.Random(8)
     keys = rand_keys(rng, 20000, 0, 64)
