@@ -13,7 +13,8 @@ step() { echo "=== $1 ($(date +%T))"; }
 printf 'FETCH_SIZE\nWRITE_SIZE\nTCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum\n' > "$OUT/traffic_groups.txt"
 for wl in single varlen; do
   step "pmc $wl"
-  OUT=$OUT/pmc_$wl GROUPS_FILE=$OUT/traffic_groups.txt BENCH_ARGS="--workload $wl" bash tools/pmc.sh || exit 1
+  GROUPS_FILE=$OUT/traffic_groups.txt OUT=$OUT/pmc_$wl BENCH_ARGS="--workload $wl" bash tools/pmc.sh || exit 1
+  ls $OUT/pmc_$wl/p1 > /dev/null || exit 1
   python3 tools/pmc_traffic.py "$OUT/pmc_$wl" profiles/pmc_traffic.json $wl > "$OUT/traffic_$wl.json" || exit 1
 done
 cp profiles/pmc_traffic.json "$OUT/pmc_traffic.json"
