@@ -211,6 +211,25 @@ def test_build_varlen_hash_pass_switch(dev, ab, oracle, monkeypatch, var_hash):
     assert np.array_equal(bm, oracle.keys2block(data.cpu().numpy(), offs.cpu().numpy().view(np.uint64)))
 
 
+@pytest.mark.parametrize("hv_keys", ["256", "1024", "2048"])
+def test_build_varlen_hashing_run_sizes(dev, ab, oracle, monkeypatch, hv_keys):
+    # the hashing pass's other run sizes (ADL_BLOOM_HV_KEYS; 512 is the default)
+    monkeypatch.setenv("ADL_BLOOM_HV_KEYS", hv_keys)
+    data, offs = ab.synth_varlen(150_001, seed=int(hv_keys))
+    bm = ab.build(data, offs).cpu().numpy()
+    assert np.array_equal(bm, oracle.keys2block(data.cpu().numpy(), offs.cpu().numpy().view(np.uint64)))
+
+
+@pytest.mark.parametrize("mode", ["1", "2"])
+def test_build_pair_table_modes(dev, ab, oracle, monkeypatch, mode):
+    # ADL_BLOOM_DD_MODE 1: every key claims its (h1, h2); 2 (default): keys with
+    # h1 == h2 claim h1.  1.5M SplitMix keys: 269 chunks, more than one round
+    monkeypatch.setenv("ADL_BLOOM_DD_MODE", mode)
+    keys = ab.synth_keys16(1_500_000, seed=0x5EED)
+    bm = ab.build(keys).cpu().numpy()
+    assert np.array_equal(bm, oracle.keys2block(keys.cpu().numpy()))
+
+
 def test_build_segmented_varlen_superchunk_edges(dev, ab, oracle):
     # filters of 4096-key hashing runs +-1, empty and 1-key filters in one launch
     rng = random.Random(12)
