@@ -84,13 +84,21 @@ __device__ __forceinline__ void store_nt(uint4 *p, uint4 v) {
 }
 
 // ---------------------------------------------------------------- scans
-// Inclusive wave64 scan.
-__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {
-#pragma unroll
-  for (int off = 1; off < kWave; off <<= 1) {
-    uint32_t t = __shfl_up(v, off, kWave);
-    if (lane >= off) v += t;
-  }
+// Inclusive wave64 scan by DPP (row shifts inside 16-lane rows, then the
+// row broadcasts 15 and 31): about 6 VALU steps instead of 6 ds_bpermute round
+// trips through the LDS.  Lanes a DPP source does not cover read 0.
+__device__ __forceinline__ uint32_t row16_incl_scan(uint32_t v) {
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);  // row_shr:1
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);  // row_shr:2
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);  // row_shr:4
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);  // row_shr:8
+  return v;
+}
+
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int /*lane*/) {
+  v = row16_incl_scan(v);
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
   return v;
 }
 
@@ -153,23 +161,21 @@ __device__ __forceinline__ uint32_t block_excl_scan_array_1b(uint32_t *a, uint32
   const uint32_t incl = wave_incl_scan(v, lane);
   if (lane == kWave - 1) scratch[wave] = incl;
   __syncthreads();
-  // the totals of waves 0..wave-1: lanes < wave hold one each (all within lanes
-  // 0..NW-1), summed over those lanes and broadcast from lane 0
+  // the totals of waves 0..wave-1: lane i < NW <= 16 holds wave i's, scanned
+  // inside the first 16-lane row; wave w reads lane w-1, the total lane NW-1
+  static_assert(NW <= 16, "wave totals scanned inside one DPP row");
   const uint32_t wt = lane < NW ? scratch[lane] : 0u;
-  uint32_t t = lane < wave ? wt : 0u, all = wt;
-#pragma unroll
-  for (int off = 1; off < NW; off <<= 1) {
-    t += __shfl_xor(t, off, kWave);
-    all += __shfl_xor(all, off, kWave);
-  }
-  uint32_t run = __builtin_amdgcn_readfirstlane(t) + incl - v;
+  const uint32_t wi = row16_incl_scan(wt);
+  const uint32_t before = wave ? __builtin_amdgcn_readlane(wi, wave - 1) : 0u;
+  const uint32_t all = __builtin_amdgcn_readlane(wi, NW - 1);
+  uint32_t run = before + incl - v;
   for (uint32_t i = beg; i < end; ++i) {
     const uint32_t x = a[i];
     a[i] = run;
     run += x;
   }
   if (per > 1) __syncthreads();
-  return __builtin_amdgcn_readfirstlane(all);
+  return all;
 }
 
 }  // namespace adl_dev
