@@ -382,7 +382,7 @@ __global__ __launch_bounds__(kBlk) void pb_bin_kernel(const uint2 *__restrict__ 
       }
     }
     __syncthreads();
-    const uint32_t total = block_excl_scan_array<kBlk>(hist, T + 1, scratch);
+    const uint32_t total = block_excl_scan_array_1b<kBlk>(hist, T + 1, scratch);
     uint32_t *tab = table + d.table_base;
     for (uint32_t t = tid; t <= T; t += kBlk) tab[(uint64_t)t * d.nchunks + j] = hist[t];
     __syncthreads();
