@@ -519,7 +519,7 @@ __global__ __launch_bounds__(kHvBlock) void hash_var_kernel(BuildArgs a, KeysVar
     o1[i] = keys.offs[kb + idx + 1];
   }
   u32x4_t v[VPT];  // (the ext-vector type: an array of uint4 held across the barrier goes to scratch)
-  {
+  if (nv) {  // a run of empty keys has no byte to stage (and maybe none to read)
     const u32x4_t *src = reinterpret_cast<const u32x4_t *>(keys.keys + base16);
 #pragma unroll
     for (int i = 0; i < VPT; ++i) v[i] = src[min((uint32_t)(tid + i * kHvBlock), nv - 1u)];

@@ -202,6 +202,14 @@ def test_build_varlen_long_and_mixed_keys(dev, ab, oracle):
     assert np.array_equal(bm, oracle.keys2block(data, offs))
 
 
+def test_build_varlen_all_empty_keys(dev, ab, oracle):
+    # runs of empty keys stage nothing; the key buffer holds no byte at all
+    keys = [b""] * 5000
+    data, offs = oracle.pack(keys)
+    bm = ab.build(to_dev(dev, data[:16]), to_dev(dev, offs.view(np.int64))).cpu().numpy()
+    assert np.array_equal(bm, oracle.keys2block(data, offs))
+
+
 @pytest.mark.parametrize("var_hash", ["0", "1"])
 def test_build_varlen_hash_pass_switch(dev, ab, oracle, monkeypatch, var_hash):
     # ADL_BLOOM_VAR_HASH=0 is the fused pass A that hashes inside the chunk loop
