@@ -557,9 +557,12 @@ __global__ __launch_bounds__(kHvBlock) void hash_var_kernel(BuildArgs a, KeysVar
     if (rk[i] != ~0u) {
       const uint32_t slot = bins[rk[i] & (kHvBins - 1)] + (rk[i] >> 9);
       const uint64_t len = o1[i] - o0[i];
-      // a key of 64 KiB or more keeps its index in the run instead of its start
-      s_rel[slot] = len < 0xffffu ? (uint32_t)(o0[i] - base16) : tid + i * kHvBlock;
-      s_len[slot] = (uint16_t)min(len, (uint64_t)0xffffu);
+      // a key of 64 KiB or more, or one starting 4 GiB or more past the run's
+      // first key, keeps its index in the run instead of its start (and is
+      // hashed from global memory)
+      const bool near = len < 0xffffu && o0[i] - base16 < 0xffffffffull;
+      s_rel[slot] = near ? (uint32_t)(o0[i] - base16) : tid + i * kHvBlock;
+      s_len[slot] = near ? (uint16_t)len : (uint16_t)0xffffu;
     }
   }
   __syncthreads();
