@@ -21,6 +21,11 @@
 //           the finished tile.  Every bitmap byte is written exactly once, so
 //           the bitmap needs no zero-fill.
 //
+// Pass A skips a key whose hash pair its workgroup already counted (the
+// reference's murmur variant repeats pairs heavily; see bloom_bin16_kernel).
+// Variable-length keys are hashed first, in length-sorted runs staged in LDS
+// (hash_var_kernel), and pass A then bins the (h1, h2) pairs.
+//
 // A direct device-scope atomicOr kernel (bloom_atomic_kernel) is kept as the
 // alternative for small filters and as an independent cross-check.
 #include <hip/hip_ext.h>
