@@ -5,6 +5,7 @@
 
 #include <mutex>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "../../include/adl_bloom.h"
 #include "murmur3_device.hpp"
@@ -290,6 +291,12 @@ struct MappedStage {
 };
 
 inline thread_local MappedStage t_mapped;
+
+// A boolean environment switch (read per call, so tests can flip it).
+inline bool env_on(const char *name, bool dflt) {
+  const char *e = getenv(name);
+  return e ? atoi(e) != 0 : dflt;
+}
 
 // The stream a synchronous host-pointer entry point runs on: the caller's, or
 // for stream == NULL a non-blocking stream of the calling thread (created on

@@ -32,6 +32,8 @@
 //    each other, and readers, like the reference's (src/db.cpp:166-172), take
 //    no lock for the duration of a lookup.
 #include <hip/hip_runtime.h>
+
+#include <chrono>
 #include <stdint.h>
 #include <string.h>
 
@@ -328,11 +330,18 @@ int adl_bloom_filter_cache_probe(adl_bloom_filter_cache *c, const char *const *o
       hbuf = sg.host;
       dbuf = sg.dev;
     }
+    // A mapped small batch is waited for by watching its answers arrive (each
+    // is written once, 0 or 1, over a 0xFF sentinel) instead of a stream
+    // synchronize: every answer present means every key and range has been
+    // read.  It falls back to the synchronize after 2 ms (or with
+    // ADL_BLOOM_SPIN=0).
+    const bool spin = hbuf != sg.host && n <= 4096 && adl_host::env_on("ADL_BLOOM_SPIN", true);
     if (rc == ADL_OK) {
       if (key_bytes) memcpy(hbuf, h_keys, key_bytes);
       if (off_bytes) memcpy(hbuf + o_offs, h_offsets, off_bytes);
       memcpy(hbuf + o_fid, h_table, n * 4);
       memcpy(hbuf + o_be, be.data(), be.size() * 8);
+      if (spin) memset(hbuf + o_out, 0xff, n);
       if (hbuf == sg.host && hipMemcpyAsync(dbuf, hbuf, o_out, hipMemcpyHostToDevice, st) != hipSuccess)
         rc = ADL_ERR_DEVICE;
     }
@@ -346,7 +355,22 @@ int adl_bloom_filter_cache_probe(adl_bloom_filter_cache *c, const char *const *o
         hipMemcpyAsync(hbuf + o_out, dbuf + o_out, n, hipMemcpyDeviceToHost, st) != hipSuccess)
       rc = ADL_ERR_DEVICE;
     // the kernel and the copies are done before any pinned range can be reused
-    if (hipStreamSynchronize(st) != hipSuccess && rc == ADL_OK) rc = ADL_ERR_DEVICE;
+    bool arrived = false;
+    if (spin && rc == ADL_OK) {
+      const volatile uint8_t *ans = hbuf + o_out;
+      const auto t0 = std::chrono::steady_clock::now();
+      uint64_t i = 0;
+      for (;;) {
+        while (i < n && ans[i] != 0xff) ++i;
+        if (i == n) {
+          arrived = true;
+          break;
+        }
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) break;
+        __builtin_ia32_pause();
+      }
+    }
+    if (!arrived && hipStreamSynchronize(st) != hipSuccess && rc == ADL_OK) rc = ADL_ERR_DEVICE;
     // 3. unpin (a range retired meanwhile is freed by its last unpin)
     unpin_all();
     if (rc) return rc;
