@@ -575,9 +575,12 @@ __global__ __launch_bounds__(kHvBlock) void hash_var_kernel(BuildArgs a, KeysVar
   // ---- hash, group g = 64 sorted slots
   const uint32_t groups = (cnt + kWave - 1) / kWave;
   uint2 *out = hp + (uint64_t)d.chunk_base * a.C + first;
-  for (uint32_t g = wave; g < groups; g += NW) {
+  // longest groups first (slots are sorted by length): the waves start on the
+  // groups that set the workgroup's end, and the short ones fill in behind
+  for (uint32_t gi = wave; gi < groups; gi += NW) {
+    const uint32_t g = groups - 1 - gi;
     const uint32_t s = g * kWave + lane;
-    if (s >= cnt) break;
+    if (s >= cnt) continue;
     uint32_t len = s_len[s];
     const uint32_t r = s_rel[s];
     uint32_t h1, h2;
