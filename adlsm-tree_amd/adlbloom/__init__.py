@@ -45,6 +45,7 @@ EXPORTS = (
     "adl_synth_varlen_lengths_device", "adl_synth_varlen_fill_device",
     "adl_bloom_profile_enable", "adl_bloom_profile_collect", "adl_synth_probe_queries_device",
     "adl_bloom_profile_each", "adl_bloom_probe_batch_workspace_bytes", "adl_bloom_probe_batch_device",
+    "adl_bloom_test_fault",
 )
 
 _LIB = None
@@ -109,6 +110,7 @@ def lib() -> ctypes.CDLL:
         "adl_bloom_profile_enable": (ctypes.c_int, [u32]),
         "adl_bloom_profile_collect": (ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(u32)]),
         "adl_bloom_profile_each": (ctypes.c_int, [ctypes.POINTER(ctypes.c_double), u32, ctypes.POINTER(u32)]),
+        "adl_bloom_test_fault": (ctypes.c_int, [ctypes.c_int, ctypes.c_int64]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -360,6 +362,16 @@ def murmur3(seed: int, data: bytes) -> int:
     _check(lib().adl_bloom_murmur3(seed, ctypes.cast(buf, ctypes.c_void_p), len(data), ctypes.byref(h)),
            "adl_bloom_murmur3")
     return h.value
+
+
+# test-only fault injection (include/adl_bloom.h, adl_bloom_test_fault)
+TEST_FAULT_PIPELINE_GROUP = 1
+TEST_FAULT_CACHE_COMPLETION = 2
+
+
+def test_fault(site: int, arg: int) -> None:
+    """Arm (arg >= 0) or disarm (arg < 0) a one-shot injected failure."""
+    _check(lib().adl_bloom_test_fault(site, arg), "adl_bloom_test_fault")
 
 
 def profile_enable(capacity: int = 4096) -> None:

@@ -35,6 +35,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <mutex>
 #include <type_traits>
 #include <vector>
@@ -51,7 +52,7 @@ constexpr int kBlockB = 1024;       // pass B threads per workgroup
 constexpr int kDepthB = 8;          // segments per pipeline stage per wave, pass B (ADL_BLOOM_DEPTH)
 constexpr int kSegBatch = 2048;     // segment descriptors staged in LDS per batch, pass B
 constexpr uint32_t kTablePad = 64;  // spare words after the table
-constexpr int kMaxFilters = 8;      // filters per launch pair (descriptors ride in kernargs)
+constexpr int kMaxFilters = 8;      // filters whose descriptors ride in the kernargs (more: a device table)
 constexpr uint32_t kHistMax = 2049; // tiles per filter + 1 (m < 2^31, TL >= ... keeps T <= 2048)
 constexpr uint32_t kMinTileLog2 = 10;
 constexpr uint32_t kMaxTileLog2 = 20;     // 128 KiB LDS tile
@@ -113,6 +114,69 @@ __device__ __forceinline__ int find_filter_by_tile(const BuildArgs &a, uint32_t 
   return f;
 }
 
+__device__ __forceinline__ int find_filter_by_run(const BuildArgs &a, uint32_t sc) {
+  int f = 0;
+#pragma unroll
+  for (int i = 1; i < kMaxFilters; ++i)
+    if ((uint32_t)i < a.nf && sc >= a.f[i].sc_base) f = i;
+  return f;
+}
+
+// A launch of more than kMaxFilters filters (a compaction's tables in one
+// launch pair) finds its descriptors in the workspace: the descriptor array
+// and, filled on the device by fill_maps_kernel, one filter index per pass-A
+// chunk, per pass-B tile and per hashing run.  Constant address space, so a
+// lookup is one scalar load.
+template <typename T>
+using cptr = const __attribute__((address_space(4))) T *;
+struct FilterTable {
+  cptr<FilterDesc> fd;
+  cptr<uint32_t> chunk_f, tile_f, sc_f;
+};
+
+template <bool DT>
+struct Filt;
+template <>
+struct Filt<false> {  // descriptors in BuildArgs::f
+  __device__ static FilterDesc at(const BuildArgs &a, const FilterTable &, int i) { return a.f[i]; }
+  __device__ static int of_chunk(const BuildArgs &a, const FilterTable &, uint32_t wg) {
+    return find_filter_by_chunk(a, wg);
+  }
+  __device__ static int of_tile(const BuildArgs &a, const FilterTable &, uint32_t wg) {
+    return find_filter_by_tile(a, wg);
+  }
+  __device__ static int of_run(const BuildArgs &a, const FilterTable &, uint32_t sc) { return find_filter_by_run(a, sc); }
+};
+template <>
+struct Filt<true> {  // descriptors in the workspace's FilterTable
+  __device__ static FilterDesc at(const BuildArgs &, const FilterTable &t, int i) {
+    static_assert(sizeof(FilterDesc) % 16 == 0, "descriptors load as whole uint4s");
+    constexpr int NV = sizeof(FilterDesc) / 16;
+    const cptr<u32x4_t> src = reinterpret_cast<cptr<u32x4_t>>(t.fd) + (uint32_t)i * NV;
+    u32x4_t v[NV];
+#pragma unroll
+    for (int j = 0; j < NV; ++j) v[j] = src[j];
+    FilterDesc d;
+    __builtin_memcpy(&d, v, sizeof(d));
+    return d;
+  }
+  __device__ static int of_chunk(const BuildArgs &, const FilterTable &t, uint32_t wg) { return (int)t.chunk_f[wg]; }
+  __device__ static int of_tile(const BuildArgs &, const FilterTable &t, uint32_t wg) { return (int)t.tile_f[wg]; }
+  __device__ static int of_run(const BuildArgs &, const FilterTable &t, uint32_t sc) { return (int)t.sc_f[sc]; }
+};
+
+// FilterTable maps: block f writes filter f's chunk, tile and run ranges.
+__global__ __launch_bounds__(256) void fill_maps_kernel(const FilterDesc *__restrict__ fd, uint32_t *__restrict__ chunk_f,
+                                                        uint32_t *__restrict__ tile_f, uint32_t *__restrict__ sc_f,
+                                                        uint32_t hv_keys) {
+  const uint32_t f = blockIdx.x;
+  const FilterDesc d = fd[f];
+  for (uint32_t i = threadIdx.x; i < d.chunks; i += 256) chunk_f[d.chunk_base + i] = f;
+  for (uint32_t i = threadIdx.x; i < d.tiles; i += 256) tile_f[d.tile_base + i] = f;
+  const uint32_t runs = (d.n + hv_keys - 1) / hv_keys;
+  for (uint32_t i = threadIdx.x; i < runs; i += 256) sc_f[d.sc_base + i] = f;
+}
+
 // ---------------------------------------------------------------- diagnostics
 // Built only with -DADL_BLOOM_STAMPS (make stamps): wave 0 of every
 // workgroup accumulates s_memtime cycles per kernel phase; read back with
@@ -162,11 +226,13 @@ struct KeyRegs<Keys16> {
 //
 // KFIX > 0: k known at compile time, positions kept in registers between the
 // count and the scatter; KFIX == 0: runtime k, positions recomputed.
-template <int BLOCK, int KFIX, int KPT, class Keys>
+template <int BLOCK, int KFIX, int KPT, class Keys, bool DT>
 __global__ __launch_bounds__(BLOCK) void bloom_bin_kernel(BuildArgs a, Keys keys,
                                                             uint32_t *__restrict__ pos_ws,
                                                             uint32_t *__restrict__ table_ws,
-                                                            uint32_t total_chunks, uint32_t *__restrict__ tile_queue) {
+                                                            uint32_t total_chunks, uint32_t *__restrict__ tile_queue,
+                                                            FilterTable ft) {
+  using FT = Filt<DT>;
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   const int tid = threadIdx.x;
   if (blockIdx.x == 0 && tid == 0) *tile_queue = 0;  // pass B's tile queue
@@ -190,7 +256,7 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin_kernel(BuildArgs a, Keys keys
 
   auto fetch = [&](uint32_t chunk, KeyRegs<Keys> (&r)[KPT]) {
     if constexpr (PF) {
-      const FilterDesc &d = a.f[find_filter_by_chunk(a, chunk)];
+      const FilterDesc d = FT::at(a, ft, FT::of_chunk(a, ft, chunk));
       const uint32_t first = (chunk - d.chunk_base) * C;
       const uint32_t cnt = min(C, d.n - first);
 #pragma unroll
@@ -221,8 +287,7 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin_kernel(BuildArgs a, Keys keys
   for (uint32_t r = 0; r < rounds; ++r) {
     const uint32_t wg = r * G + slot;
     if (wg >= total_chunks) break;  // only the last round is partial
-    const int fi = find_filter_by_chunk(a, wg);
-    const FilterDesc &d = a.f[fi];
+    const FilterDesc d = FT::at(a, ft, FT::of_chunk(a, ft, wg));
     const uint32_t w = wg - d.chunk_base;
     const uint32_t first = w * C;
     const uint32_t cnt = min(C, d.n - first);
@@ -482,9 +547,9 @@ constexpr size_t hv_lds_bytes() {
   return kHvBins * 4 + S * 4 + S * 2 + hv_stage_bytes<S>() + 16;
 }
 
-template <uint32_t S>
+template <uint32_t S, bool DT>
 __global__ __launch_bounds__(kHvBlock) void hash_var_kernel(BuildArgs a, KeysVar keys, uint2 *__restrict__ hp,
-                                                            uint32_t total_sc) {
+                                                            uint32_t total_sc, FilterTable ft) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   uint32_t *bins = lds;                                             // kHvBins
   uint32_t *s_rel = lds + kHvBins;                                  // key start - base16, by sorted slot
@@ -495,11 +560,7 @@ __global__ __launch_bounds__(kHvBlock) void hash_var_kernel(BuildArgs a, KeysVar
   const int tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid / kWave;
   const uint32_t sc = blockIdx.x;
   if (sc >= total_sc) return;
-  int fi = 0;
-#pragma unroll
-  for (int i = 1; i < kMaxFilters; ++i)
-    if ((uint32_t)i < a.nf && sc >= a.f[i].sc_base) fi = i;
-  const FilterDesc &d = a.f[fi];
+  const FilterDesc d = Filt<DT>::at(a, ft, Filt<DT>::of_run(a, ft, sc));
   const uint32_t first = (sc - d.sc_base) * S;
   const uint32_t cnt = min(S, d.n - first);
   const uint64_t kb = d.key_begin + first;
@@ -633,11 +694,13 @@ struct SrcH {
 //   prefetch keys of c+2
 // so the murmur work hides under the scatter's LDS latency and the position
 // stores drain under the next count.
-template <int BLOCK, int K, class Src>
+template <int BLOCK, int K, class Src, bool DT>
 __global__ __launch_bounds__(BLOCK) void bloom_bin16_kernel(BuildArgs a, Src keys,
                                                               uint32_t *__restrict__ pos_ws,
                                                               uint32_t *__restrict__ table_ws,
-                                                              uint32_t total_chunks, uint32_t *__restrict__ tile_queue) {
+                                                              uint32_t total_chunks, uint32_t *__restrict__ tile_queue,
+                                                              FilterTable ft) {
+  using FT = Filt<DT>;
   constexpr int KPT = 6;                    // keys per thread (C <= 6 * BLOCK)
   constexpr int VPT = (K * KPT + 3) / 4;    // 16-byte stores per thread per chunk, at most
   constexpr int SPI = (VPT + KPT - 1) / KPT;  // of those, per count iteration
@@ -668,7 +731,7 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin16_kernel(BuildArgs a, Src key
 
   using Raw = typename Src::Raw;
   auto fetch = [&](uint32_t chunk, Raw (&raw)[KPT]) {
-    const FilterDesc &d = a.f[find_filter_by_chunk(a, chunk)];
+    const FilterDesc d = FT::at(a, ft, FT::of_chunk(a, ft, chunk));
     const uint32_t first = (chunk - d.chunk_base) * C;
     const uint32_t last = min(C, d.n - first) - 1u;
 #pragma unroll
@@ -711,8 +774,8 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin16_kernel(BuildArgs a, Src key
   uint32_t ptotal = 0;
   STAMP_DECL
   for (uint32_t wg = slot; wg < total_chunks; wg += G) {
-    const int fcur = find_filter_by_chunk(a, wg);
-    const FilterDesc &d = a.f[fcur];
+    const int fcur = FT::of_chunk(a, ft, wg);
+    const FilterDesc d = FT::at(a, ft, fcur);
     const uint32_t w = wg - d.chunk_base;
     const uint32_t cnt = min(C, d.n - w * C);
     const uint32_t T = d.tiles;
@@ -813,7 +876,7 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin16_kernel(BuildArgs a, Src key
     STAMP(4);
     for (uint32_t i = tid; i <= T; i += BLOCK) hist[i] = 0;
     // the pair table holds one filter's pairs (positions depend on m)
-    if (dd && wg + G < total_chunks && find_filter_by_chunk(a, wg + G) != fcur)
+    if (dd && wg + G < total_chunks && FT::of_chunk(a, ft, wg + G) != fcur)
       for (uint32_t i = tid; i < (1u << dd); i += BLOCK) dtab[i] = kEmpty;
     pdst = reinterpret_cast<uint4 *>(pos_ws + d.pos_base + (uint64_t)w * a.cap);
     ptotal = total;
@@ -840,12 +903,14 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin16_kernel(BuildArgs a, Src key
 // while the current stage is ds_or_b32'd into the LDS tile.  The rare longer
 // segments (hot tiles) finish in a 4-deep unrolled loop.  The finished tile's
 // 16-byte stores drain while the next tile is zeroed.
-template <int D>
+template <int D, bool DT>
 __global__ __launch_bounds__(kBlockB) void bloom_tile_kernel(BuildArgs a,
                                                              const uint32_t *__restrict__ pos_ws,
                                                              const uint32_t *__restrict__ table_ws,
                                                              uint8_t *__restrict__ bitmaps,
-                                                             uint32_t total_tiles, uint32_t *__restrict__ tile_queue) {
+                                                             uint32_t total_tiles, uint32_t *__restrict__ tile_queue,
+                                                             FilterTable ft) {
+  using FT = Filt<DT>;
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   const int tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid / kWave;
   constexpr int NWAVES = kBlockB / kWave;
@@ -856,8 +921,8 @@ __global__ __launch_bounds__(kBlockB) void bloom_tile_kernel(BuildArgs a,
   uint2 *seg = reinterpret_cast<uint2 *>(lds + tile_words);  // kSegBatch {start word, length}
   uint32_t *qs = lds + tile_words + 2 * kSegBatch;           // tile-queue broadcast (2 words)
 
-  auto fetch_rows = [&](uint32_t wg, uint32_t wb, uint32_t (&rs)[RPT], uint32_t (&re)[RPT]) {
-    const FilterDesc &d = a.f[find_filter_by_tile(a, wg)];
+  // d: the descriptor of tile wg's filter
+  auto fetch_rows = [&](const FilterDesc &d, uint32_t wg, uint32_t wb, uint32_t (&rs)[RPT], uint32_t (&re)[RPT]) {
     const uint32_t lt = wg - d.tile_base, W = d.chunks;
     const uint32_t *row0 = table_ws + d.table_base + (uint64_t)lt * W;
 #pragma unroll
@@ -900,7 +965,13 @@ __global__ __launch_bounds__(kBlockB) void bloom_tile_kernel(BuildArgs a,
     wg = (a.xcd_remap && G % 8 == 0) ? (blockIdx.x % 8) * (G / 8) + blockIdx.x / 8 : blockIdx.x;
   }
   uint32_t pre_s[RPT], pre_e[RPT];
-  if (wg < total_tiles) fetch_rows(wg, 0, pre_s, pre_e);
+  // the descriptor of the current tile's filter; the next tile's is looked up
+  // at the top of the current one, so its (scalar) loads land during the gather
+  FilterDesc dcur{};
+  if (wg < total_tiles) {
+    dcur = FT::at(a, ft, FT::of_tile(a, ft, wg));
+    fetch_rows(dcur, wg, 0, pre_s, pre_e);
+  }
   {  // the tile starts zeroed; every write-out re-zeroes it
     uint4 *t4w = reinterpret_cast<uint4 *>(tile);
     for (uint32_t i = tid; i < tile_words / 4; i += kBlockB) t4w[i] = make_uint4(0, 0, 0, 0);
@@ -908,7 +979,7 @@ __global__ __launch_bounds__(kBlockB) void bloom_tile_kernel(BuildArgs a,
   STAMP_DECL
 
   while (wg < total_tiles) {
-    const FilterDesc &d = a.f[find_filter_by_tile(a, wg)];
+    const FilterDesc d = dcur;
     const uint32_t lt = wg - d.tile_base;
     const uint32_t W = d.chunks;
     const uint32_t pos_base = (uint32_t)d.pos_base;
@@ -917,8 +988,9 @@ __global__ __launch_bounds__(kBlockB) void bloom_tile_kernel(BuildArgs a,
     __syncthreads();  // next tile index published
     STAMP(0);
     const uint32_t next = a.dyn_tiles ? qs[1] : wg + G;
+    const FilterDesc dnext = next < total_tiles ? FT::at(a, ft, FT::of_tile(a, ft, next)) : d;
     // an empty filter (no chunks) has no batch to prefetch the next tile from
-    if (W == 0 && next < total_tiles) fetch_rows(next, 0, pre_s, pre_e);
+    if (W == 0 && next < total_tiles) fetch_rows(dnext, next, 0, pre_s, pre_e);
 
     for (uint32_t wb = 0; wb < W; wb += kSegBatch) {
       const uint32_t nw = min((uint32_t)kSegBatch, W - wb);
@@ -927,7 +999,7 @@ __global__ __launch_bounds__(kBlockB) void bloom_tile_kernel(BuildArgs a,
 #pragma unroll
         for (int r = 0; r < RPT; ++r) rs[r] = pre_s[r], re[r] = pre_e[r];
       } else {
-        fetch_rows(wg, wb, rs, re);
+        fetch_rows(d, wg, wb, rs, re);
       }
 #pragma unroll
       for (int r = 0; r < RPT; ++r) {
@@ -936,7 +1008,7 @@ __global__ __launch_bounds__(kBlockB) void bloom_tile_kernel(BuildArgs a,
       }
       __syncthreads();  // segment list ready
       STAMP(1);
-      if (wb + kSegBatch >= W && next < total_tiles) fetch_rows(next, 0, pre_s, pre_e);
+      if (wb + kSegBatch >= W && next < total_tiles) fetch_rows(dnext, next, 0, pre_s, pre_e);
 
       const uint32_t Q = nw > (uint32_t)wave ? (nw - wave + NWAVES - 1) / NWAVES : 0;
       struct Stage {
@@ -1029,6 +1101,7 @@ __global__ __launch_bounds__(kBlockB) void bloom_tile_kernel(BuildArgs a,
     __syncthreads();  // the tile is read out and zero again
     STAMP(3);
     wg = next;
+    dcur = dnext;
   }
 #ifdef ADL_BLOOM_STAMPS
   if (exp_sink == 0x9e3779b9u) tile_queue[1] = exp_sink;  // keeps the diagnostic sum alive
@@ -1067,7 +1140,9 @@ inline KeysVar shift_keys(KeysVar k, uint64_t b) { k.offs += b; return k; }
 // ---------------------------------------------------------------- host plan
 struct Plan {
   BuildArgs a;
-  uint64_t pos_words = 0, table_words = 0, scratch_words = 0, hash_words = 0, ws_bytes = 0;
+  std::vector<FilterDesc> f;  // every filter's descriptor (a.f holds them too when nf <= kMaxFilters)
+  bool dt = false;            // more than kMaxFilters: descriptors in the workspace's FilterTable
+  uint64_t pos_words = 0, table_words = 0, scratch_words = 0, hash_words = 0, ft_bytes = 0, ws_bytes = 0;
   uint32_t total_chunks = 0, total_tiles = 0, total_sc = 0;
   uint32_t grid_a = 0, grid_b = 0;  // persistent grids
   uint32_t block_a = 512;             // pass A threads per workgroup
@@ -1087,8 +1162,10 @@ uint32_t env_u32(const char *name, uint32_t dflt) {
 }
 
 int make_plan(const uint64_t *counts, uint32_t nf, int32_t bpk, Plan &p) {
-  if (nf == 0 || nf > (uint32_t)kMaxFilters || bpk < 0) return ADL_ERR_INVALID_ARG;
+  if (nf == 0 || bpk < 0) return ADL_ERR_INVALID_ARG;
   memset(&p.a, 0, sizeof(p.a));
+  p.f.assign(nf, FilterDesc{});
+  p.dt = nf > (uint32_t)kMaxFilters;
   const uint32_t k = (uint32_t)adl_host::num_probes(bpk);
   uint64_t total_n = 0;
   for (uint32_t f = 0; f < nf; ++f) {
@@ -1134,12 +1211,20 @@ int make_plan(const uint64_t *counts, uint32_t nf, int32_t bpk, Plan &p) {
   const uint32_t cmax =
       std::min<uint32_t>(block_a * kpt, (lds_words_a - hist_words - 32 - 256) / (k + 1)) & ~3u;
   if (cmax < 4) return ADL_ERR_TOO_LARGE;
-  const uint64_t wmin = (total_n + cmax - 1) / cmax;
+  // chunks of C keys over all filters (each filter's last chunk is partial)
+  auto nchunks = [&](uint64_t c) {
+    uint64_t w = 0;
+    for (uint32_t f = 0; f < nf; ++f) w += (counts[f] + c - 1) / c;
+    return w;
+  };
+  const uint64_t wmin = nchunks(cmax);
   uint32_t C;
   if (wmin >= grid_a_max) {
     const uint64_t rounds = (wmin + grid_a_max - 1) / grid_a_max;
     C = (uint32_t)std::min<uint64_t>(
         cmax, adl_host::round_up((total_n + rounds * grid_a_max - 1) / (rounds * grid_a_max), 4));
+    // the smallest C whose chunks, rounded up per filter, still fill no more rounds
+    while (C + 4 <= cmax && nchunks(C) > rounds * grid_a_max) C += 4;
   } else {
     C = (uint32_t)std::min<uint64_t>(
         cmax, std::max<uint64_t>(256, adl_host::round_up((total_n + grid_a_max - 1) / grid_a_max, 4)));
@@ -1179,7 +1264,7 @@ int make_plan(const uint64_t *counts, uint32_t nf, int32_t bpk, Plan &p) {
   uint64_t pos = 0, tab = 0, boff = 0;
   uint32_t chunk = 0, tile = 0, sc = 0;
   for (uint32_t f = 0; f < nf; ++f) {
-    FilterDesc &d = p.a.f[f];
+    FilterDesc &d = p.f[f];
     const uint64_t bytes = adl_host::bitmap_bytes(counts[f], bpk);
     const uint32_t m = (uint32_t)(bytes * 8);
     d.n = (uint32_t)counts[f];
@@ -1202,6 +1287,7 @@ int make_plan(const uint64_t *counts, uint32_t nf, int32_t bpk, Plan &p) {
     tab += (uint64_t)(d.tiles + 1) * d.chunks;
   }
   if (pos + 64 >= (1ull << 32)) return ADL_ERR_TOO_LARGE;  // u32 position indices
+  if (!p.dt) std::copy(p.f.begin(), p.f.end(), p.a.f);
   p.total_chunks = chunk;
   p.total_tiles = tile;
   p.total_sc = sc;
@@ -1214,7 +1300,9 @@ int make_plan(const uint64_t *counts, uint32_t nf, int32_t bpk, Plan &p) {
   // (variable-length keys; reserved for every key shape so the workspace size
   // does not depend on it)
   p.hash_words = adl_host::round_up(2ull * chunk * C, 64);
-  p.ws_bytes = (p.pos_words + p.table_words + p.scratch_words + p.hash_words) * 4 + 256;
+  // then (more than kMaxFilters) the FilterTable: descriptors, chunk / tile / run maps
+  p.ft_bytes = p.dt ? adl_host::round_up(nf * sizeof(FilterDesc), 256) + 4ull * (chunk + tile + sc) + 256 : 0;
+  p.ws_bytes = (p.pos_words + p.table_words + p.scratch_words + p.hash_words) * 4 + p.ft_bytes + 256;
   p.lds_a = (size_t)(hist_words + 32 + (k + 1) * C + 256) * 4;
   p.lds_b = (size_t)((1u << (TL - 5)) + 2 * kSegBatch + 4) * 4;
   p.grid_a = std::min<uint32_t>(p.total_chunks, grid_a_max);
@@ -1251,92 +1339,116 @@ inline hipEvent_t *prof_slot() {
   return &t_prof.ev[4 * t_prof.used++];
 }
 
-template <class Keys>
-int launch_binned(const Plan &p, Keys keys, uint8_t *d_bitmaps, void *ws, hipStream_t st) {
+template <bool DT, class Keys>
+int launch_binned_dt(const Plan &p, Keys keys, uint8_t *d_bitmaps, void *ws, hipStream_t st) {
   uint32_t *pos_ws = reinterpret_cast<uint32_t *>(ws);
   uint32_t *tab_ws = pos_ws + p.pos_words;
   uint32_t *queue = tab_ws + p.table_words;  // pass B tile queue, then pass A's scratch lines
+  uint2 *hp = reinterpret_cast<uint2 *>(queue + p.scratch_words);
+  FilterTable ft{};
+  if constexpr (DT) {
+    // the descriptors go up in stream order; the maps are filled on the device
+    uint8_t *fbase = reinterpret_cast<uint8_t *>(queue + p.scratch_words + p.hash_words);
+    FilterDesc *fd = reinterpret_cast<FilterDesc *>(fbase);
+    uint32_t *chunk_f = reinterpret_cast<uint32_t *>(fbase + adl_host::round_up(p.f.size() * sizeof(FilterDesc), 256));
+    uint32_t *tile_f = chunk_f + p.total_chunks, *sc_f = tile_f + p.total_tiles;
+    if (int rc = adl_host::t_upload.upload(fd, p.f.data(), p.f.size() * sizeof(FilterDesc), st)) return rc;
+    hipLaunchKernelGGL(fill_maps_kernel, dim3((uint32_t)p.f.size()), dim3(256), 0, st, fd, chunk_f, tile_f, sc_f,
+                       p.a.hv_keys);
+    ADL_HIP_TRY(hipGetLastError());
+    ft.fd = (cptr<FilterDesc>)fd;
+    ft.chunk_f = (cptr<uint32_t>)chunk_f;
+    ft.tile_f = (cptr<uint32_t>)tile_f;
+    ft.sc_f = (cptr<uint32_t>)sc_f;
+  }
   hipEvent_t *ev = prof_slot();
   if (ev && !p.total_chunks) {  // no pass A: an empty interval
     ADL_HIP_TRY(hipEventRecord(ev[0], st));
     ADL_HIP_TRY(hipEventRecord(ev[1], st));
   }
   if (p.total_chunks) {
-    uint2 *hp = reinterpret_cast<uint2 *>(queue + p.scratch_words);
-    auto go_src = [&](auto kern, auto src, bool hashed) -> int {
-      ADL_HIP_TRY(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      (int)p.lds_a));
+    // lim: lds_limit<kern>; the hashing pass (var-len keys) before pass A opens
+    // the profiled pass-A interval instead of it
+    auto go_src = [&](auto lim, auto kern, const BuildArgs &args, auto src, bool hashed) -> int {
+      if (int rc = lim()) return rc;
       hipExtLaunchKernelGGL(kern, dim3(p.grid_a), dim3(p.block_a), p.lds_a, st,
-                            ev && !hashed ? ev[0] : nullptr, ev ? ev[1] : nullptr, 0, p.a, src, pos_ws, tab_ws,
-                            p.total_chunks, queue);
+                            ev && !hashed ? ev[0] : nullptr, ev ? ev[1] : nullptr, 0, args, src, pos_ws, tab_ws,
+                            p.total_chunks, queue, ft);
       ADL_HIP_TRY(hipGetLastError());
       return ADL_OK;
     };
-    auto go = [&](auto kern) -> int { return go_src(kern, keys, false); };
-    auto by_block = [&](auto k6, auto kgen) -> int {  // k6/kgen: tag types carrying BLOCK
-      constexpr int B = decltype(k6)::value;
+    auto by_block = [&](auto bt) -> int {  // bt: tag type carrying BLOCK
+      constexpr int B = decltype(bt)::value;
       if constexpr (std::is_same<Keys, Keys16>::value) {
         if (p.a.k == 6 && !p.sequential_a && !p.a.dedup)
-          return go_src(bloom_bin16_kernel<B, 6, Src16>, Src16{keys.keys}, false);
+          return go_src(adl_host::lds_limit<bloom_bin16_kernel<B, 6, Src16, DT>>, bloom_bin16_kernel<B, 6, Src16, DT>,
+                        p.a, Src16{keys.keys}, false);
       }
       if constexpr (std::is_same<Keys, KeysVar>::value) {
         // length-sorted hashing pass, then pass A over the (h1, h2) pairs; the
         // profiled pass-A interval spans both launches
         if (p.a.k == 6 && p.a.var_hash && !p.sequential_a && !p.a.dedup) {
-          auto hv_go = [&](auto kern, size_t lds) -> int {
-            ADL_HIP_TRY(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                            (int)lds));
+          auto hv_go = [&](auto lim, auto kern, size_t lds) -> int {
+            if (int rc = lim()) return rc;
             hipExtLaunchKernelGGL(kern, dim3(p.total_sc), dim3(kHvBlock), lds, st, ev ? ev[0] : nullptr, nullptr, 0,
-                                  p.a, keys, hp, p.total_sc);
+                                  p.a, keys, hp, p.total_sc, ft);
             ADL_HIP_TRY(hipGetLastError());
             return ADL_OK;
           };
-          const int rh = p.a.hv_keys == 256    ? hv_go(hash_var_kernel<256>, hv_lds_bytes<256>())
-                         : p.a.hv_keys == 512  ? hv_go(hash_var_kernel<512>, hv_lds_bytes<512>())
-                         : p.a.hv_keys == 1024 ? hv_go(hash_var_kernel<1024>, hv_lds_bytes<1024>())
-                                               : hv_go(hash_var_kernel<2048>, hv_lds_bytes<2048>());
+          const int rh = p.a.hv_keys == 256
+                             ? hv_go(adl_host::lds_limit<hash_var_kernel<256, DT>>, hash_var_kernel<256, DT>,
+                                     hv_lds_bytes<256>())
+                         : p.a.hv_keys == 512
+                             ? hv_go(adl_host::lds_limit<hash_var_kernel<512, DT>>, hash_var_kernel<512, DT>,
+                                     hv_lds_bytes<512>())
+                         : p.a.hv_keys == 1024
+                             ? hv_go(adl_host::lds_limit<hash_var_kernel<1024, DT>>, hash_var_kernel<1024, DT>,
+                                     hv_lds_bytes<1024>())
+                             : hv_go(adl_host::lds_limit<hash_var_kernel<2048, DT>>, hash_var_kernel<2048, DT>,
+                                     hv_lds_bytes<2048>());
           if (rh) return rh;
           // the pair table pays for 16-byte keys only (configs[2]'s keys repeat few pairs:
           // pass B 64 -> 70 us with it)
           BuildArgs av = p.a;
           av.dd_log2 = 0;
-          ADL_HIP_TRY(hipFuncSetAttribute((const void *)bloom_bin16_kernel<B, 6, SrcH>,
-                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)p.lds_a));
-          hipExtLaunchKernelGGL(bloom_bin16_kernel<B, 6, SrcH>, dim3(p.grid_a), dim3(p.block_a), p.lds_a, st, nullptr,
-                                ev ? ev[1] : nullptr, 0, av, SrcH{hp, p.a.C}, pos_ws, tab_ws, p.total_chunks, queue);
-          ADL_HIP_TRY(hipGetLastError());
-          return ADL_OK;
+          return go_src(adl_host::lds_limit<bloom_bin16_kernel<B, 6, SrcH, DT>>, bloom_bin16_kernel<B, 6, SrcH, DT>,
+                        av, SrcH{hp, p.a.C}, true);
         }
       }
-      if (p.a.k == 6) return go(bloom_bin_kernel<B, 6, 6, Keys>);
-      return go(bloom_bin_kernel<B, 0, kKptMax, Keys>);
+      if (p.a.k == 6)
+        return go_src(adl_host::lds_limit<bloom_bin_kernel<B, 6, 6, Keys, DT>>, bloom_bin_kernel<B, 6, 6, Keys, DT>,
+                      p.a, keys, false);
+      return go_src(adl_host::lds_limit<bloom_bin_kernel<B, 0, kKptMax, Keys, DT>>,
+                    bloom_bin_kernel<B, 0, kKptMax, Keys, DT>, p.a, keys, false);
     };
-    const int rc = p.block_a == 1024 ? by_block(std::integral_constant<int, 1024>{}, 0)
-                                     : by_block(std::integral_constant<int, 512>{}, 0);
+    const int rc = p.block_a == 1024 ? by_block(std::integral_constant<int, 1024>{})
+                                     : by_block(std::integral_constant<int, 512>{});
     if (rc) return rc;
   }
-  auto go_b = [&](auto kern) -> int {
-    ADL_HIP_TRY(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)p.lds_b));
-    BuildArgs ab = p.a;
-    if (!p.total_chunks) ab.dyn_tiles = 0;  // no pass A ran to reset the queue
+  BuildArgs ab = p.a;
+  if (!p.total_chunks) ab.dyn_tiles = 0;  // no pass A ran to reset the queue
+  auto go_b = [&](auto lim, auto kern) -> int {
+    if (int rc = lim()) return rc;
     hipExtLaunchKernelGGL(kern, dim3(p.grid_b), dim3(kBlockB), p.lds_b, st, ev ? ev[2] : nullptr,
                           ev ? ev[3] : nullptr, 0, ab, (const uint32_t *)pos_ws, (const uint32_t *)tab_ws,
-                          d_bitmaps, p.total_tiles, queue);
+                          d_bitmaps, p.total_tiles, queue, ft);
     ADL_HIP_TRY(hipGetLastError());
     return ADL_OK;
   };
-  int rcb;
-  if (p.depth <= 4) rcb = go_b(bloom_tile_kernel<4>);
-  else if (p.depth <= 6) rcb = go_b(bloom_tile_kernel<6>);
-  else if (p.depth <= 8) rcb = go_b(bloom_tile_kernel<8>);
-  else rcb = go_b(bloom_tile_kernel<12>);
-  return rcb;
+  if (p.depth <= 4) return go_b(adl_host::lds_limit<bloom_tile_kernel<4, DT>>, bloom_tile_kernel<4, DT>);
+  if (p.depth <= 6) return go_b(adl_host::lds_limit<bloom_tile_kernel<6, DT>>, bloom_tile_kernel<6, DT>);
+  if (p.depth <= 8) return go_b(adl_host::lds_limit<bloom_tile_kernel<8, DT>>, bloom_tile_kernel<8, DT>);
+  return go_b(adl_host::lds_limit<bloom_tile_kernel<12, DT>>, bloom_tile_kernel<12, DT>);
+}
+
+template <class Keys>
+int launch_binned(const Plan &p, Keys keys, uint8_t *d_bitmaps, void *ws, hipStream_t st) {
+  return p.dt ? launch_binned_dt<true>(p, keys, d_bitmaps, ws, st) : launch_binned_dt<false>(p, keys, d_bitmaps, ws, st);
 }
 
 template <class Keys>
 int launch_atomic(const Plan &p, Keys keys, uint8_t *d_bitmaps, hipStream_t st) {
-  for (uint32_t f = 0; f < p.a.nf; ++f) {
-    const FilterDesc &d = p.a.f[f];
+  for (const FilterDesc &d : p.f) {
     const uint64_t n16 = d.alloc_bytes / 16;
     hipLaunchKernelGGL(zero_kernel, dim3((uint32_t)std::min<uint64_t>((n16 + 255) / 256, 4096)), dim3(256), 0,
                        st, reinterpret_cast<uint4 *>(d_bitmaps + d.bitmap_off), n16);
@@ -1356,7 +1468,11 @@ int launch_atomic(const Plan &p, Keys keys, uint8_t *d_bitmaps, hipStream_t st) 
 }  // namespace
 
 namespace {
-// Runs groups of <= kMaxFilters filters through the plan/launch pair.
+// Runs the filters through the plan/launch pair: all in one launch pair (a
+// compaction's tables), split only where the u32 position indices of one
+// launch's workspace would overflow (groups of at most 2^31 / k keys).
+uint64_t group_keys_max(int32_t bpk) { return (1ull << 31) / (uint64_t)adl_host::num_probes(bpk); }
+
 int build_groups(const uint8_t *d_keys, const uint64_t *d_offsets, uint32_t key_stride,
                  const uint64_t *key_begin, uint32_t num_filters, int32_t bpk, uint8_t *d_bitmaps,
                  const uint64_t *bitmap_off, void *d_workspace, uint64_t workspace_bytes,
@@ -1364,22 +1480,31 @@ int build_groups(const uint8_t *d_keys, const uint64_t *d_offsets, uint32_t key_
   if (flags & ~(uint32_t)ADL_BLOOM_SKIP_ADJACENT_DUPLICATES) return ADL_ERR_INVALID_ARG;
   if (!d_keys && key_begin[num_filters] > key_begin[0]) return ADL_ERR_INVALID_ARG;
   if (!d_offsets && key_stride == 0 && key_begin[num_filters] > key_begin[0]) return ADL_ERR_INVALID_ARG;
+  if (bpk < 0) return ADL_ERR_INVALID_ARG;
   const bool atomic = use_atomic_path();
-  for (uint32_t g = 0; g < num_filters; g += kMaxFilters) {
-    const uint32_t nf = std::min<uint32_t>(kMaxFilters, num_filters - g);
-    uint64_t counts[kMaxFilters];
-    for (uint32_t f = 0; f < nf; ++f) {
-      if (key_begin[g + f + 1] < key_begin[g + f]) return ADL_ERR_INVALID_ARG;
-      counts[f] = key_begin[g + f + 1] - key_begin[g + f];
+  const uint64_t gmax = group_keys_max(bpk);
+  std::vector<uint64_t> counts;
+  for (uint32_t g = 0; g < num_filters;) {
+    counts.clear();
+    uint64_t keys_in = 0;
+    uint32_t e = g;
+    for (; e < num_filters; ++e) {
+      if (key_begin[e + 1] < key_begin[e]) return ADL_ERR_INVALID_ARG;
+      const uint64_t c = key_begin[e + 1] - key_begin[e];
+      if (e > g && keys_in + c > gmax) break;
+      counts.push_back(c);
+      keys_in += c;
     }
+    const uint32_t nf = e - g;
     Plan p;
-    int rc = make_plan(counts, nf, bpk, p);
+    int rc = make_plan(counts.data(), nf, bpk, p);
     if (rc) return rc;
     p.a.dedup = (flags & ADL_BLOOM_SKIP_ADJACENT_DUPLICATES) ? 1u : 0u;
     for (uint32_t f = 0; f < nf; ++f) {
       if (bitmap_off[g + f] % 16) return ADL_ERR_INVALID_ARG;
-      p.a.f[f].key_begin = key_begin[g + f];
-      p.a.f[f].bitmap_off = bitmap_off[g + f];
+      p.f[f].key_begin = key_begin[g + f];
+      p.f[f].bitmap_off = bitmap_off[g + f];
+      if (!p.dt) p.a.f[f] = p.f[f];
     }
     if (!atomic && (!d_workspace || workspace_bytes < p.ws_bytes)) return ADL_ERR_WORKSPACE;
     void *ws = d_workspace;
@@ -1396,6 +1521,7 @@ int build_groups(const uint8_t *d_keys, const uint64_t *d_offsets, uint32_t key_
       rc = atomic ? launch_atomic(p, keys, d_bitmaps, st) : launch_binned(p, keys, d_bitmaps, ws, st);
     }
     if (rc) return rc;
+    g = e;
   }
   return ADL_OK;
 }
@@ -1418,6 +1544,12 @@ const char *adl_bloom_strerror(int status) {
 }
 
 int adl_bloom_abi_version(void) { return ADL_BLOOM_ABI_VERSION; }
+
+int adl_bloom_test_fault(int site, int64_t arg) {
+  if (site != ADL_TEST_FAULT_PIPELINE_GROUP && site != ADL_TEST_FAULT_CACHE_COMPLETION) return ADL_ERR_INVALID_ARG;
+  adl_host::g_test_faults.site[site].store(arg < 0 ? -1 : arg);
+  return ADL_OK;
+}
 
 #ifdef ADL_BLOOM_STAMPS
 // Diagnostics build only: copies g_stamps ([pass][workgroup][phase] cycles).
@@ -1443,12 +1575,21 @@ uint64_t adl_bloom_bitmap_alloc_bytes(uint64_t n, int32_t bits_per_key) {
 uint64_t adl_bloom_build_workspace_bytes(const uint64_t *key_counts, uint32_t num_filters,
                                          int32_t bits_per_key) {
   if (!key_counts) return 0;
+  if (bits_per_key < 0) return 0;
+  // the same grouping as build_groups
+  const uint64_t gmax = group_keys_max(bits_per_key);
   uint64_t ws = 0;
-  for (uint32_t g = 0; g < num_filters; g += kMaxFilters) {
-    const uint32_t nf = std::min<uint32_t>(kMaxFilters, num_filters - g);
+  for (uint32_t g = 0; g < num_filters;) {
+    uint64_t keys_in = 0;
+    uint32_t e = g;
+    for (; e < num_filters; ++e) {
+      if (e > g && keys_in + key_counts[e] > gmax) break;
+      keys_in += key_counts[e];
+    }
     Plan p;
-    if (make_plan(key_counts + g, nf, bits_per_key, p)) return 0;
+    if (make_plan(key_counts + g, e - g, bits_per_key, p)) return 0;
     ws = std::max(ws, p.ws_bytes);
+    g = e;
   }
   return ws;
 }

@@ -3,9 +3,11 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <mutex>
 #include <stdint.h>
 #include <stdlib.h>
+#include <string.h>
 
 #include "../../include/adl_bloom.h"
 #include "murmur3_device.hpp"
@@ -321,5 +323,72 @@ struct ThreadStream {
 inline thread_local ThreadStream t_stream;
 
 inline hipStream_t sync_stream(void *stream) { return stream ? (hipStream_t)stream : t_stream.get(); }
+
+// Small host -> device uploads in stream order from pinned memory (a build's
+// filter descriptors): a ring of slots per thread, each reused only after its
+// previous copy has completed.
+struct UploadRing {
+  static constexpr int kSlots = 4;
+  uint8_t *host[kSlots] = {};
+  uint64_t cap[kSlots] = {};
+  hipEvent_t ev[kSlots] = {};
+  bool used[kSlots] = {};
+  int next = 0;
+  ~UploadRing() {
+    for (int s = 0; s < kSlots; ++s) {
+      if (used[s]) (void)hipEventSynchronize(ev[s]);
+      if (ev[s]) (void)hipEventDestroy(ev[s]);
+      if (host[s]) (void)hipHostFree(host[s]);
+    }
+  }
+  int upload(void *dst, const void *src, uint64_t bytes, hipStream_t st) {
+    const int s = next;
+    next = (next + 1) % kSlots;
+    if (!ev[s]) ADL_HIP_TRY(hipEventCreateWithFlags(&ev[s], hipEventDisableTiming));
+    if (used[s]) ADL_HIP_TRY(hipEventSynchronize(ev[s]));
+    used[s] = false;
+    if (bytes > cap[s]) {
+      if (host[s]) (void)hipHostFree(host[s]);
+      host[s] = nullptr;
+      cap[s] = 0;
+      const uint64_t want = round_up(bytes, 1 << 16);
+      ADL_HIP_TRY(hipHostMalloc((void **)&host[s], want, hipHostMallocDefault));
+      cap[s] = want;
+    }
+    memcpy(host[s], src, bytes);
+    ADL_HIP_TRY(hipMemcpyAsync(dst, host[s], bytes, hipMemcpyHostToDevice, st));
+    ADL_HIP_TRY(hipEventRecord(ev[s], st));
+    used[s] = true;
+    return ADL_OK;
+  }
+};
+
+inline thread_local UploadRing t_upload;
+
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per kernel and device
+// (the whole 160 KiB of a CU; each launch asks for what it uses), not on every
+// launch.
+template <auto Kern>
+int lds_limit() {
+  static std::atomic<uint64_t> done{0};
+  int dev = 0;
+  ADL_HIP_TRY(hipGetDevice(&dev));
+  const uint64_t bit = 1ull << (dev & 63);
+  if (done.load(std::memory_order_acquire) & bit) return ADL_OK;
+  ADL_HIP_TRY(hipFuncSetAttribute((const void *)Kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+  done.fetch_or(bit, std::memory_order_acq_rel);
+  return ADL_OK;
+}
+
+// adl_bloom_test_fault's armed sites (-1: off).  take() disarms and returns the
+// argument, so an armed fault fires once.
+struct TestFaults {
+  std::atomic<int64_t> site[3] = {-1, -1, -1};
+  int64_t take(int s) {
+    if (site[s].load(std::memory_order_relaxed) < 0) return -1;
+    return site[s].exchange(-1);
+  }
+};
+inline TestFaults g_test_faults;
 
 }  // namespace adl_host

@@ -5,7 +5,7 @@
 // SSTables, src/db.cpp:428-509, each finalised by SSTableWriter::Final ->
 // FilterBlockWriter::Final, src/sstable.cpp:58) hands over keys in host
 // memory and wants the bitmaps back in host memory.  The filters are taken in
-// groups (<= kGroupFilters filters, <= kGroupKeyBytes of keys); group g's keys
+// groups (about kGroupKeyBytes of keys each, one launch pair per group); group g's keys
 // upload on one stream while group g-1 builds on the caller's stream and group
 // g-2's bitmaps download on a third, so the end-to-end rate approaches the
 // slower PCIe direction instead of the sum of both plus the kernels.
@@ -24,8 +24,8 @@
 
 namespace {
 
-constexpr uint32_t kGroupFilters = 8;               // filters per launch pair (bloom_build.hip kMaxFilters)
-constexpr uint64_t kGroupKeyBytes = 32ull << 20;    // keys per group, soft cap (at least one filter)
+// keys per group, soft cap (at least one filter); ADL_BLOOM_PIPE_MB overrides
+constexpr uint64_t kGroupKeyBytes = 128ull << 20;  // measured: 32 MB 166 ms, 128 MB 76 ms, 512 MB 114 ms
 
 bool is_pinned(const void *p) {
   if (!p) return false;
@@ -128,14 +128,15 @@ extern "C" int adl_bloom_build_segmented(const uint8_t *h_keys, const uint64_t *
     auto key_byte = [&](uint64_t k) -> uint64_t { return h_offsets ? h_offsets[k] : k * (uint64_t)key_stride; };
 
     // groups of consecutive filters
+    const char *mb_env = getenv("ADL_BLOOM_PIPE_MB");
+    const uint64_t group_bytes = mb_env && atoll(mb_env) > 0 ? (uint64_t)atoll(mb_env) << 20 : kGroupKeyBytes;
     std::vector<Group> groups;
     uint64_t max_in = 0, max_out = 0, max_ws = 0;
     for (uint32_t f0 = 0; f0 < num_filters;) {
       Group g{};
       g.f0 = f0;
       uint32_t f1 = f0 + 1;
-      while (f1 < num_filters && f1 - f0 < kGroupFilters &&
-             key_byte(key_begin[f1 + 1]) - key_byte(key_begin[f0]) <= kGroupKeyBytes)
+      while (f1 < num_filters && key_byte(key_begin[f1 + 1]) - key_byte(key_begin[f0]) <= group_bytes)
         ++f1;
       g.f1 = f1;
       g.k0 = key_begin[f0];
@@ -182,10 +183,9 @@ extern "C" int adl_bloom_build_segmented(const uint8_t *h_keys, const uint64_t *
       P.ws_cap = max_ws;
     }
     P.used_up[0] = P.used_up[1] = P.used_down[0] = P.used_down[1] = false;
-    // fault injection for the error-path tests: group g's build fails
-    // (ADL_BLOOM_FAULT_GROUP=g), with earlier groups' copies still in flight
-    const char *fault_env = getenv("ADL_BLOOM_FAULT_GROUP");
-    const long fault_group = fault_env ? atol(fault_env) : -1;
+    // fault injection for the error-path tests (adl_bloom_test_fault): group
+    // g's build fails, with earlier groups' copies still in flight
+    const int64_t fault_group = adl_host::g_test_faults.take(ADL_TEST_FAULT_PIPELINE_GROUP);
 
     std::vector<uint64_t> local_kb, dev_off;
     // host side of a finished group: copy its bitmaps out of the pinned staging

@@ -64,6 +64,24 @@ int parse_block(const uint8_t *b, uint64_t len, int32_t want_bpk, std::vector<ui
   return ADL_OK;
 }
 
+// The calling thread's completion event of a mapped small-batch probe (timing
+// off: it is only queried).
+struct DoneEvent {
+  hipEvent_t e = nullptr;
+  bool tried = false;
+  ~DoneEvent() {
+    if (e) (void)hipEventDestroy(e);
+  }
+  hipEvent_t get() {
+    if (!tried) {
+      tried = true;
+      if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) e = nullptr;
+    }
+    return e;
+  }
+};
+thread_local DoneEvent t_done;
+
 }  // namespace
 
 struct adl_bloom_filter_cache {
@@ -331,10 +349,12 @@ int adl_bloom_filter_cache_probe(adl_bloom_filter_cache *c, const char *const *o
       dbuf = sg.dev;
     }
     // A mapped small batch is waited for by watching its answers arrive (each
-    // is written once, 0 or 1, over a 0xFF sentinel) instead of a stream
-    // synchronize: every answer present means every key and range has been
-    // read.  It falls back to the synchronize after 2 ms (or with
-    // ADL_BLOOM_SPIN=0).
+    // is written once, 0 or 1, over a 0xFF sentinel, by bloom_probe_multi_kernel's
+    // one store per query after all its reads) instead of a stream
+    // synchronize.  The pinned ranges are released only once the launch's
+    // completion event has fired too, so a fault after the answers landed is
+    // still this call's error.  Both waits fall back to the synchronize after
+    // 2 ms (or with ADL_BLOOM_SPIN=0).
     const bool spin = hbuf != sg.host && n <= 4096 && adl_host::env_on("ADL_BLOOM_SPIN", true);
     if (rc == ADL_OK) {
       if (key_bytes) memcpy(hbuf, h_keys, key_bytes);
@@ -354,23 +374,38 @@ int adl_bloom_filter_cache_probe(adl_bloom_filter_cache *c, const char *const *o
     if (rc == ADL_OK && hbuf == sg.host &&
         hipMemcpyAsync(hbuf + o_out, dbuf + o_out, n, hipMemcpyDeviceToHost, st) != hipSuccess)
       rc = ADL_ERR_DEVICE;
+    hipEvent_t done = spin && rc == ADL_OK ? t_done.get() : nullptr;
+    if (done && hipEventRecord(done, st) != hipSuccess) done = nullptr;
     // the kernel and the copies are done before any pinned range can be reused
-    bool arrived = false;
-    if (spin && rc == ADL_OK) {
+    bool finished = false;
+    if (done) {
       const volatile uint8_t *ans = hbuf + o_out;
       const auto t0 = std::chrono::steady_clock::now();
+      auto late = [&] { return std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2); };
       uint64_t i = 0;
       for (;;) {
         while (i < n && ans[i] != 0xff) ++i;
-        if (i == n) {
-          arrived = true;
-          break;
-        }
-        if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) break;
+        if (i == n || late()) break;
         __builtin_ia32_pause();
       }
+      if (i == n) {  // every answer is in: now the launch itself
+        const bool fault = adl_host::g_test_faults.take(ADL_TEST_FAULT_CACHE_COMPLETION) >= 0;
+        for (;;) {
+          const hipError_t q = fault ? hipErrorLaunchFailure : hipEventQuery(done);
+          if (q == hipSuccess) {
+            finished = true;
+            break;
+          }
+          if (q != hipErrorNotReady) {
+            rc = ADL_ERR_DEVICE;
+            break;
+          }
+          if (late()) break;
+          __builtin_ia32_pause();
+        }
+      }
     }
-    if (!arrived && hipStreamSynchronize(st) != hipSuccess && rc == ADL_OK) rc = ADL_ERR_DEVICE;
+    if (!finished && hipStreamSynchronize(st) != hipSuccess && rc == ADL_OK) rc = ADL_ERR_DEVICE;
     // 3. unpin (a range retired meanwhile is freed by its last unpin)
     unpin_all();
     if (rc) return rc;

@@ -722,23 +722,20 @@ int adl_bloom_probe_batch_device(const uint8_t *d_keys, const uint64_t *d_offset
     hipLaunchKernelGGL(pb_scan_kernel, dim3(F + 1), dim3(kBlk), 0, st, cnt, start, p.nb, F, p.C, p.maxch, desc, cf,
                        scal);
     ADL_HIP_TRY(hipGetLastError());
-    ADL_HIP_TRY(hipFuncSetAttribute((const void *)pb_scatter_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    (int)lds_k3));
+    if (int rc = adl_host::lds_limit<pb_scatter_kernel>()) return rc;
     hipLaunchKernelGGL(pb_scatter_kernel, dim3(p.nb), dim3(kBlk), lds_k3, st, reinterpret_cast<const uint4 *>(d_keys),
                        d_filter_id, n, F, p.nb, desc, cnt, start, dest, hs);
     ADL_HIP_TRY(hipGetLastError());
     auto p1 = p.k == 6 ? pb_bin_kernel<6> : pb_bin_kernel<0>;
-    ADL_HIP_TRY(hipFuncSetAttribute((const void *)p1, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_p1));
+    if (int rc = p.k == 6 ? adl_host::lds_limit<pb_bin_kernel<6>>() : adl_host::lds_limit<pb_bin_kernel<0>>()) return rc;
     hipLaunchKernelGGL(p1, dim3(cus), dim3(kBlk), lds_p1, st, hs, desc, cf, scal, p.k, p.C, ent, tab, res);
     ADL_HIP_TRY(hipGetLastError());
-    ADL_HIP_TRY(hipFuncSetAttribute((const void *)pb_tile_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    (int)lds_p2));
+    if (int rc = adl_host::lds_limit<pb_tile_kernel>()) return rc;
     const char *exp_env = getenv("ADL_PB_EXP");  // diagnostics build only
     hipLaunchKernelGGL(pb_tile_kernel, dim3(cus), dim3(kBlk), lds_p2, st, d_bitmaps, desc, F, scal, p.k, p.C, ent,
                        tab, res, exp_env ? (uint32_t)atoi(exp_env) : 0u);
     ADL_HIP_TRY(hipGetLastError());
-    ADL_HIP_TRY(hipFuncSetAttribute((const void *)pb_gather_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    (int)lds_k6));
+    if (int rc = adl_host::lds_limit<pb_gather_kernel>()) return rc;
     hipLaunchKernelGGL(pb_gather_kernel, dim3(p.nb), dim3(kBlk), lds_k6, st, dest, res, n, F, p.nb, cnt, start,
                        d_out);
     ADL_HIP_TRY(hipGetLastError());

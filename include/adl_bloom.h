@@ -311,6 +311,16 @@ int adl_bloom_profile_collect(double *ms, uint32_t *builds);
  * medians); call before adl_bloom_profile_collect. */
 int adl_bloom_profile_each(double *ms_ab, uint32_t capacity, uint32_t *launch_pairs);
 
+/* Test-only fault injection (the error-path tests; never set by the product).
+ * ADL_TEST_FAULT_PIPELINE_GROUP, arg g >= 0: the next adl_bloom_build_segmented
+ * call fails in its group g's build, with earlier groups' copies in flight.
+ * ADL_TEST_FAULT_CACHE_COMPLETION, arg >= 0: the next filter-cache probe that
+ * waits for its answers in the mapped buffer sees its kernel's completion
+ * report a device error after all answers have arrived.  arg < 0 disarms. */
+#define ADL_TEST_FAULT_PIPELINE_GROUP 1
+#define ADL_TEST_FAULT_CACHE_COMPLETION 2
+int adl_bloom_test_fault(int site, int64_t arg);
+
 /* ---------------------------------------------------------------- synthetic data */
 
 /* SURVEY.md §8d SplitMix64 16-byte keys, generated on the device: key i of the

@@ -140,6 +140,81 @@ def test_filter_cache_concurrent_put_probe(dev, ab, oracle):
     assert not errors, errors[:5]
 
 
+def test_filter_cache_small_batch_under_eviction(dev, ab, oracle):
+    """Small batches (<= 4096 keys: the mapped buffer, answers watched instead
+    of a stream synchronize) from 4 threads while a churn thread puts tables
+    into a cache that holds about 6 of them, so probed tables are evicted while
+    probes pin them.  An uncached table answers 1 ("may be present"); a
+    range released too early would answer 0 for an inserted key."""
+    T = 8
+    tabs = [_block(oracle, 2000 + t, 20_000) for t in range(T)]
+    blk_bytes = len(tabs[0][1])
+    cache = ab.FilterCache(6 * blk_bytes + (64 << 10), max_tables=64)
+    oids = [b"ev-%02d" % t for t in range(T)]
+    rng = np.random.default_rng(11)
+    n = 3000
+    table = rng.integers(0, T, n).astype(np.uint32)
+    fresh = oracle.splitmix_keys16(0xBEEF, n)
+    q = np.where((rng.integers(0, 2, n) == 1)[:, None],
+                 np.stack([tabs[t][0][(7 * i) % 20_000] for i, t in enumerate(table)]), fresh)
+    want = np.empty(n, np.uint8)
+    for t in range(T):
+        sel = table == t
+        want[sel] = oracle.probe(q[sel], oracle.keys2block(tabs[t][0]))
+    errors, exact = [], [0]
+    stop = threading.Event()
+
+    def prober(k):
+        for r in range(40):
+            got, unc = cache.probe(oids, table, q)
+            if np.any(got < want) or (unc == 0 and not np.array_equal(got, want)):
+                errors.append((k, r, int(unc), int((got < want).sum())))
+            exact[0] += unc == 0
+
+    def churn():
+        i = 0
+        while not stop.is_set():
+            cache.put(oids[i % T], tabs[i % T][1])
+            cache.put(b"filler-%d" % (i % 3), tabs[(i + 3) % T][1])
+            i += 1
+
+    for o, (_, blk) in zip(oids[:6], tabs[:6]):
+        cache.put(o, blk)
+    th = [threading.Thread(target=prober, args=(k,)) for k in range(4)]
+    ch = threading.Thread(target=churn)
+    for t in th + [ch]:
+        t.start()
+    for t in th:
+        t.join()
+    stop.set()
+    ch.join()
+    cache.close()
+    assert not errors, errors[:5]
+
+
+def test_filter_cache_completion_fault(dev, ab, oracle):
+    """A small batch whose launch reports an error after every answer has
+    arrived in the mapped buffer fails (it does not return those answers), and
+    the next call on the same thread is exact again."""
+    keys, blk = _block(oracle, 3000, 20_000)
+    cache = ab.FilterCache(8 << 20, max_tables=8)
+    cache.put(b"t0", blk)
+    q = np.concatenate([keys[:500], oracle.splitmix_keys16(0xCAFE, 500)])
+    table = np.zeros(len(q), np.uint32)
+    want = oracle.probe(q, oracle.keys2block(keys))
+    got, unc = cache.probe([b"t0"], table, q)
+    assert unc == 0 and np.array_equal(got, want)
+    ab.test_fault(ab.TEST_FAULT_CACHE_COMPLETION, 0)
+    try:
+        with pytest.raises(ab.AdlBloomError):
+            cache.probe([b"t0"], table, q)
+    finally:
+        ab.test_fault(ab.TEST_FAULT_CACHE_COMPLETION, -1)
+    got, unc = cache.probe([b"t0"], table, q)
+    assert unc == 0 and np.array_equal(got, want)
+    cache.close()
+
+
 @pytest.mark.parametrize("stride", [8, 24])
 def test_pipeline_fixed_stride_unaligned_groups(dev, ab, oracle, stride):
     """adl_bloom_build_segmented with fixed-stride keys: more than 8 filters (so
@@ -161,10 +236,10 @@ def test_pipeline_fixed_stride_unaligned_groups(dev, ab, oracle, stride):
 
 @pytest.mark.parametrize("pinned", [False, True])
 def test_pipeline_fault_mid_pipeline(dev, ab, oracle, monkeypatch, pinned):
-    """A build failing in group 2 (ADL_BLOOM_FAULT_GROUP) returns the error only
+    """A build failing in group 2 (adl_bloom_test_fault) returns the error only
     after every copy into the caller's buffer has finished: the buffer does not
     change after the call returns.  The next call succeeds."""
-    sizes = [400_000] * 24  # 3 groups of 8 filters
+    sizes = [400_000] * 24  # 5 groups (32 MB of keys each)
     kb = np.concatenate([[0], np.cumsum(sizes)]).astype(np.uint64)
     hk = oracle.splitmix_keys16(99, int(kb[-1]))
     nbytes = [ab.bitmap_bytes(s, 10) for s in sizes]
@@ -177,13 +252,16 @@ def test_pipeline_fault_mid_pipeline(dev, ab, oracle, monkeypatch, pinned):
     else:
         keys, out = hk, np.zeros(total, dtype=np.uint8)
         view = lambda: out.copy()  # noqa: E731
-    monkeypatch.setenv("ADL_BLOOM_FAULT_GROUP", "2")
-    with pytest.raises(ab.AdlBloomError):
-        ab.build_segmented_host(keys, kb, out, boff)
+    monkeypatch.setenv("ADL_BLOOM_PIPE_MB", "32")  # groups of 5 filters: group 2 exists
+    ab.test_fault(ab.TEST_FAULT_PIPELINE_GROUP, 2)
+    try:
+        with pytest.raises(ab.AdlBloomError):
+            ab.build_segmented_host(keys, kb, out, boff)
+    finally:
+        ab.test_fault(ab.TEST_FAULT_PIPELINE_GROUP, -1)
     a = view()
     time.sleep(0.2)
     assert np.array_equal(a, view()), "the caller's buffer changed after the error returned"
-    monkeypatch.delenv("ADL_BLOOM_FAULT_GROUP")
     ab.build_segmented_host(keys, kb, out, boff)
     full = view()
     for f in (0, 9, 23):
