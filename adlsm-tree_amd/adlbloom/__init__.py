@@ -45,7 +45,7 @@ EXPORTS = (
     "adl_synth_varlen_lengths_device", "adl_synth_varlen_fill_device",
     "adl_bloom_profile_enable", "adl_bloom_profile_collect", "adl_synth_probe_queries_device",
     "adl_bloom_profile_each", "adl_bloom_probe_batch_workspace_bytes", "adl_bloom_probe_batch_device",
-    "adl_bloom_test_fault",
+    "adl_bloom_test_fault", "adl_bloom_build_positions",
 )
 
 _LIB = None
@@ -111,6 +111,7 @@ def lib() -> ctypes.CDLL:
         "adl_bloom_profile_collect": (ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(u32)]),
         "adl_bloom_profile_each": (ctypes.c_int, [ctypes.POINTER(ctypes.c_double), u32, ctypes.POINTER(u32)]),
         "adl_bloom_test_fault": (ctypes.c_int, [ctypes.c_int, ctypes.c_int64]),
+        "adl_bloom_build_positions": (ctypes.c_int, [vp, u32, i32, vp, ctypes.POINTER(u64), vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -188,6 +189,14 @@ class Builder:
         self.ws_bytes = workspace_bytes([self.n], self.bpk)
         self.ws = empty_device(self.ws_bytes, device)
 
+    def positions(self, stream=None) -> int:
+        """Positions (bit-sets after repeated pairs were skipped) the last build wrote."""
+        cnt = np.array([self.n], dtype=np.uint64)
+        v = ctypes.c_uint64()
+        _check(lib().adl_bloom_build_positions(cnt.ctypes.data, 1, self.bpk, _dptr(self.ws), ctypes.byref(v),
+                                               _stream(stream)), "adl_bloom_build_positions")
+        return v.value
+
     def build(self, keys, offsets=None, stream=None):
         pk, po, n, stride = _keyset(keys, offsets)
         assert n == self.n
@@ -221,6 +230,14 @@ class SegmentedBuilder:
                                                       self.boff.ctypes.data, _dptr(self.ws), self.ws_bytes,
                                                       _stream(stream)), "adl_bloom_build_segmented_device")
         return self.out
+
+    def positions(self, stream=None) -> int:
+        """Positions (bit-sets after repeated pairs were skipped) the last build wrote."""
+        counts = np.ascontiguousarray(self.kb[1:] - self.kb[:-1], dtype=np.uint64)
+        v = ctypes.c_uint64()
+        _check(lib().adl_bloom_build_positions(counts.ctypes.data, len(counts), self.bpk, _dptr(self.ws),
+                                               ctypes.byref(v), _stream(stream)), "adl_bloom_build_positions")
+        return v.value
 
     def bitmap(self, f: int):
         o = int(self.boff[f])

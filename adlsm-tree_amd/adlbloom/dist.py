@@ -68,7 +68,12 @@ def owner_table(num_tables: int, world: int):
     return own, t - first[own]
 
 
-def route_probe(keys, fid, owner, local_id, probe_fn, group=None, comm_cpu=None):
+# bytes a routed query moves each way (route_probe): key + local filter id out,
+# the answer back
+ROUTE_BYTES_OUT, ROUTE_BYTES_BACK = 16 + 4, 1
+
+
+def route_probe(keys, fid, owner, local_id, probe_fn, group=None, comm_cpu=None, stats=None):
     """Multi-get across ranks: this rank's queries (keys (n, 16) uint8, fid (n,)
     global table ids) are bucketed by the rank owning each table (stable, as
     partition_queries), sent there (all_to_all), probed against the owner's
@@ -77,6 +82,8 @@ def route_probe(keys, fid, owner, local_id, probe_fn, group=None, comm_cpu=None)
     owner / local_id: per-table tensors on keys' device (owner_table).
     comm_cpu: stage the exchanges through host memory (default: when the
     backend is gloo, which moves host tensors; RCCL moves device memory).
+    stats: an optional dict that receives this rank's off-rank traffic of the
+    call (queries sent to other ranks, bytes out and back).
     Returns (answers uint8 (n,), queries this rank probed for others)."""
     import torch
     import torch.distributed as dist
@@ -95,6 +102,12 @@ def route_probe(keys, fid, owner, local_id, probe_fn, group=None, comm_cpu=None)
     dist.all_to_all_single(rcounts, xfer(counts), group=group)
     send = counts.tolist()
     recv = rcounts.tolist()
+    if stats is not None:
+        me = dist.get_rank(group)
+        off = sum(c for r, c in enumerate(send) if r != me)
+        stats.update(queries_sent_offrank=off, bytes_out=off * ROUTE_BYTES_OUT,
+                     bytes_back_in=off * ROUTE_BYTES_BACK,
+                     queries_received=sum(c for r, c in enumerate(recv) if r != me))
     # keys as 2 x int64 per query (16 B), local filter ids as int32
     k_send = keys[order].contiguous().view(torch.int64).view(-1, 2)
     f_send = local_id[fid[order]].to(torch.int32)

@@ -138,7 +138,9 @@ template <bool DT>
 struct Filt;
 template <>
 struct Filt<false> {  // descriptors in BuildArgs::f
-  __device__ static FilterDesc at(const BuildArgs &a, const FilterTable &, int i) { return a.f[i]; }
+  // a reference into the kernarg segment: fields load from it as needed (a
+  // copy of a dynamically indexed kernarg element goes through scratch)
+  __device__ static const FilterDesc &at(const BuildArgs &a, const FilterTable &, int i) { return a.f[i]; }
   __device__ static int of_chunk(const BuildArgs &a, const FilterTable &, uint32_t wg) {
     return find_filter_by_chunk(a, wg);
   }
@@ -256,7 +258,7 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin_kernel(BuildArgs a, Keys keys
 
   auto fetch = [&](uint32_t chunk, KeyRegs<Keys> (&r)[KPT]) {
     if constexpr (PF) {
-      const FilterDesc d = FT::at(a, ft, FT::of_chunk(a, ft, chunk));
+      const auto &d = FT::at(a, ft, FT::of_chunk(a, ft, chunk));
       const uint32_t first = (chunk - d.chunk_base) * C;
       const uint32_t cnt = min(C, d.n - first);
 #pragma unroll
@@ -287,7 +289,7 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin_kernel(BuildArgs a, Keys keys
   for (uint32_t r = 0; r < rounds; ++r) {
     const uint32_t wg = r * G + slot;
     if (wg >= total_chunks) break;  // only the last round is partial
-    const FilterDesc d = FT::at(a, ft, FT::of_chunk(a, ft, wg));
+    const auto &d = FT::at(a, ft, FT::of_chunk(a, ft, wg));
     const uint32_t w = wg - d.chunk_base;
     const uint32_t first = w * C;
     const uint32_t cnt = min(C, d.n - first);
@@ -560,14 +562,16 @@ __global__ __launch_bounds__(kHvBlock) void hash_var_kernel(BuildArgs a, KeysVar
   const int tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid / kWave;
   const uint32_t sc = blockIdx.x;
   if (sc >= total_sc) return;
-  const FilterDesc d = Filt<DT>::at(a, ft, Filt<DT>::of_run(a, ft, sc));
+  const auto &d = Filt<DT>::at(a, ft, Filt<DT>::of_run(a, ft, sc));
   const uint32_t first = (sc - d.sc_base) * S;
   const uint32_t cnt = min(S, d.n - first);
   const uint64_t kb = d.key_begin + first;
   const uint64_t base16 = keys.offs[kb] & ~15ull;
   const uint64_t end = keys.offs[kb + cnt];
-  // staged: bytes [base16, base16 + sbytes), whole 16-byte blocks, each
-  // holding at least one byte of the run (so every load is in bounds)
+  // staged: bytes [base16, base16 + sbytes), whole 16-byte blocks of the
+  // (16-byte-aligned) key buffer, each holding at least one byte of the run:
+  // up to 15 bytes past the run's last key are read, never a block the key
+  // bytes do not touch (include/adl_bloom.h)
   constexpr uint32_t kStage = hv_stage_bytes<S>();
   const uint32_t sbytes = (uint32_t)min((end - base16 + 15) & ~15ull, (uint64_t)kStage);
 
@@ -731,7 +735,7 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin16_kernel(BuildArgs a, Src key
 
   using Raw = typename Src::Raw;
   auto fetch = [&](uint32_t chunk, Raw (&raw)[KPT]) {
-    const FilterDesc d = FT::at(a, ft, FT::of_chunk(a, ft, chunk));
+    const auto &d = FT::at(a, ft, FT::of_chunk(a, ft, chunk));
     const uint32_t first = (chunk - d.chunk_base) * C;
     const uint32_t last = min(C, d.n - first) - 1u;
 #pragma unroll
@@ -775,7 +779,7 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin16_kernel(BuildArgs a, Src key
   STAMP_DECL
   for (uint32_t wg = slot; wg < total_chunks; wg += G) {
     const int fcur = FT::of_chunk(a, ft, wg);
-    const FilterDesc d = FT::at(a, ft, fcur);
+    const auto &d = FT::at(a, ft, fcur);
     const uint32_t w = wg - d.chunk_base;
     const uint32_t cnt = min(C, d.n - w * C);
     const uint32_t T = d.tiles;
@@ -921,8 +925,8 @@ __global__ __launch_bounds__(kBlockB) void bloom_tile_kernel(BuildArgs a,
   uint2 *seg = reinterpret_cast<uint2 *>(lds + tile_words);  // kSegBatch {start word, length}
   uint32_t *qs = lds + tile_words + 2 * kSegBatch;           // tile-queue broadcast (2 words)
 
-  // d: the descriptor of tile wg's filter
-  auto fetch_rows = [&](const FilterDesc &d, uint32_t wg, uint32_t wb, uint32_t (&rs)[RPT], uint32_t (&re)[RPT]) {
+  auto fetch_rows = [&](uint32_t wg, uint32_t wb, uint32_t (&rs)[RPT], uint32_t (&re)[RPT]) {
+    const auto &d = FT::at(a, ft, FT::of_tile(a, ft, wg));
     const uint32_t lt = wg - d.tile_base, W = d.chunks;
     const uint32_t *row0 = table_ws + d.table_base + (uint64_t)lt * W;
 #pragma unroll
@@ -965,13 +969,7 @@ __global__ __launch_bounds__(kBlockB) void bloom_tile_kernel(BuildArgs a,
     wg = (a.xcd_remap && G % 8 == 0) ? (blockIdx.x % 8) * (G / 8) + blockIdx.x / 8 : blockIdx.x;
   }
   uint32_t pre_s[RPT], pre_e[RPT];
-  // the descriptor of the current tile's filter; the next tile's is looked up
-  // at the top of the current one, so its (scalar) loads land during the gather
-  FilterDesc dcur{};
-  if (wg < total_tiles) {
-    dcur = FT::at(a, ft, FT::of_tile(a, ft, wg));
-    fetch_rows(dcur, wg, 0, pre_s, pre_e);
-  }
+  if (wg < total_tiles) fetch_rows(wg, 0, pre_s, pre_e);
   {  // the tile starts zeroed; every write-out re-zeroes it
     uint4 *t4w = reinterpret_cast<uint4 *>(tile);
     for (uint32_t i = tid; i < tile_words / 4; i += kBlockB) t4w[i] = make_uint4(0, 0, 0, 0);
@@ -979,7 +977,7 @@ __global__ __launch_bounds__(kBlockB) void bloom_tile_kernel(BuildArgs a,
   STAMP_DECL
 
   while (wg < total_tiles) {
-    const FilterDesc d = dcur;
+    const auto &d = FT::at(a, ft, FT::of_tile(a, ft, wg));
     const uint32_t lt = wg - d.tile_base;
     const uint32_t W = d.chunks;
     const uint32_t pos_base = (uint32_t)d.pos_base;
@@ -988,9 +986,8 @@ __global__ __launch_bounds__(kBlockB) void bloom_tile_kernel(BuildArgs a,
     __syncthreads();  // next tile index published
     STAMP(0);
     const uint32_t next = a.dyn_tiles ? qs[1] : wg + G;
-    const FilterDesc dnext = next < total_tiles ? FT::at(a, ft, FT::of_tile(a, ft, next)) : d;
     // an empty filter (no chunks) has no batch to prefetch the next tile from
-    if (W == 0 && next < total_tiles) fetch_rows(dnext, next, 0, pre_s, pre_e);
+    if (W == 0 && next < total_tiles) fetch_rows(next, 0, pre_s, pre_e);
 
     for (uint32_t wb = 0; wb < W; wb += kSegBatch) {
       const uint32_t nw = min((uint32_t)kSegBatch, W - wb);
@@ -999,7 +996,7 @@ __global__ __launch_bounds__(kBlockB) void bloom_tile_kernel(BuildArgs a,
 #pragma unroll
         for (int r = 0; r < RPT; ++r) rs[r] = pre_s[r], re[r] = pre_e[r];
       } else {
-        fetch_rows(d, wg, wb, rs, re);
+        fetch_rows(wg, wb, rs, re);
       }
 #pragma unroll
       for (int r = 0; r < RPT; ++r) {
@@ -1008,7 +1005,7 @@ __global__ __launch_bounds__(kBlockB) void bloom_tile_kernel(BuildArgs a,
       }
       __syncthreads();  // segment list ready
       STAMP(1);
-      if (wb + kSegBatch >= W && next < total_tiles) fetch_rows(dnext, next, 0, pre_s, pre_e);
+      if (wb + kSegBatch >= W && next < total_tiles) fetch_rows(next, 0, pre_s, pre_e);
 
       const uint32_t Q = nw > (uint32_t)wave ? (nw - wave + NWAVES - 1) / NWAVES : 0;
       struct Stage {
@@ -1101,7 +1098,6 @@ __global__ __launch_bounds__(kBlockB) void bloom_tile_kernel(BuildArgs a,
     __syncthreads();  // the tile is read out and zero again
     STAMP(3);
     wg = next;
-    dcur = dnext;
   }
 #ifdef ADL_BLOOM_STAMPS
   if (exp_sink == 0x9e3779b9u) tile_queue[1] = exp_sink;  // keeps the diagnostic sum alive
@@ -1511,7 +1507,9 @@ int build_groups(const uint8_t *d_keys, const uint64_t *d_offsets, uint32_t key_
     if (ws) ws = reinterpret_cast<void *>(adl_host::round_up(reinterpret_cast<uintptr_t>(ws), 256));
     if (d_offsets) {
       KeysVar keys{d_keys, d_offsets};
-      if (reinterpret_cast<uintptr_t>(d_keys) % 16) p.a.stage_keys = 0;  // staging loads are 16-byte
+      // staging loads (pass A's windows and the hashing pass) read whole aligned
+      // 16-byte blocks: only of a 16-byte-aligned key buffer
+      if (reinterpret_cast<uintptr_t>(d_keys) % 16) p.a.stage_keys = p.a.var_hash = 0;
       rc = atomic ? launch_atomic(p, keys, d_bitmaps, st) : launch_binned(p, keys, d_bitmaps, ws, st);
     } else if (key_stride == 16 && (reinterpret_cast<uintptr_t>(d_keys) % 16) == 0) {
       Keys16 keys{reinterpret_cast<const uint4 *>(d_keys)};
@@ -1592,6 +1590,47 @@ uint64_t adl_bloom_build_workspace_bytes(const uint64_t *key_counts, uint32_t nu
     g = e;
   }
   return ws;
+}
+
+int adl_bloom_build_positions(const uint64_t *key_counts, uint32_t num_filters, int32_t bits_per_key,
+                              const void *d_workspace, uint64_t *positions, void *stream) {
+  try {
+    if (!key_counts || !d_workspace || !positions || num_filters == 0 || bits_per_key < 0)
+      return ADL_ERR_INVALID_ARG;
+    // the last group of build_groups' grouping is what the workspace holds
+    const uint64_t gmax = group_keys_max(bits_per_key);
+    uint32_t g = 0;
+    for (uint32_t g0 = 0; g0 < num_filters;) {
+      uint64_t keys_in = 0;
+      uint32_t e = g0;
+      for (; e < num_filters; ++e) {
+        if (e > g0 && keys_in + key_counts[e] > gmax) break;
+        keys_in += key_counts[e];
+      }
+      g = g0;
+      g0 = e;
+    }
+    Plan p;
+    if (int rc = make_plan(key_counts + g, num_filters - g, bits_per_key, p)) return rc;
+    const uint32_t *tab = reinterpret_cast<const uint32_t *>(
+                              adl_host::round_up(reinterpret_cast<uintptr_t>(d_workspace), 256)) +
+                          p.pos_words;
+    hipStream_t st = adl_host::sync_stream(stream);
+    uint64_t sum = 0;
+    std::vector<uint32_t> row;
+    for (const FilterDesc &d : p.f) {  // row T of each filter's table: every chunk's total
+      row.resize(d.chunks);
+      if (!d.chunks) continue;
+      ADL_HIP_TRY(hipMemcpyAsync(row.data(), tab + d.table_base + (uint64_t)d.tiles * d.chunks, d.chunks * 4ull,
+                                 hipMemcpyDeviceToHost, st));
+      ADL_HIP_TRY(hipStreamSynchronize(st));
+      for (uint32_t v : row) sum += v;
+    }
+    *positions = sum;
+    return ADL_OK;
+  } catch (...) {
+    return ADL_ERR_DEVICE;
+  }
 }
 
 int adl_bloom_build_device(const uint8_t *d_keys, const uint64_t *d_offsets, uint64_t n,

@@ -270,12 +270,22 @@ FilterCache *FilterCache::Shared(int bits_per_key) {
   static std::map<int, FilterCache *> *caches = new std::map<int, FilterCache *>;  // kept until exit
   std::lock_guard<std::mutex> g(mu);
   FilterCache *&c = (*caches)[bits_per_key];
+  if (c && c->status() != OK) {  // an arena that could not be created is retried, not kept
+    delete c;
+    c = nullptr;
+  }
   if (!c) {
     uint64_t bytes = 1ull << 30;
     if (const char *e = getenv("ADL_BLOOM_READER_CACHE_BYTES")) bytes = strtoull(e, nullptr, 10);
-    c = new FilterCache(bytes, 1u << 20, bits_per_key);
+    // less free device memory (other processes on the GPU): a quarter, then a sixteenth
+    for (int i = 0; i < 3; ++i, bytes /= 4) {
+      c = new FilterCache(bytes, 1u << 20, bits_per_key);
+      if (c->status() == OK) break;
+      delete c;
+      c = nullptr;
+    }
   }
-  return c->status() == OK ? c : nullptr;
+  return c;
 }
 
 // ------------------------------------------------------------- FilterBlockReader
@@ -314,7 +324,7 @@ RC FilterBlockReader::Parse(string_view filter_blocks) {
 RC FilterBlockReader::Init(string_view filter_blocks) {
   if (RC rc = Parse(filter_blocks); rc) return rc;
   FilterCache *c = FilterCache::Shared(bits_per_key_);
-  if (!c) return DEVICE_ERROR;
+  if (!c) return Upload();  // no shared arena: a device copy of its own
   static std::atomic<uint64_t> next_id{0};
   oid_ = "\x01reader:" + std::to_string(next_id.fetch_add(1));
   const RC rc = c->Put(oid_, filter_blocks_);

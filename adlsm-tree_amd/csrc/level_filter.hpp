@@ -65,6 +65,11 @@ struct MultiGetFilterResult {
  * src/file_util.hpp:163-165) iterated in reverse (src/revision.cpp:278).
  * user_keys: the batch; seq: the lookup's sequence (DB::Get reads
  * sequence_id_, src/db.cpp:168).  One cache probe for all pairs. */
+/* The candidate selection of LevelMultiGetFilter alone (host only): key i's
+ * candidate tables are table[begin[i] .. begin[i+1]), in visiting order. */
+void LevelCandidates(const vector<TableRange> &tables, const vector<string_view> &user_keys, int64_t seq,
+                     vector<uint32_t> &begin, vector<uint32_t> &table);
+
 RC LevelMultiGetFilter(FilterCache &cache, const vector<TableRange> &tables, const vector<string_view> &user_keys,
                        int64_t seq, MultiGetFilterResult &out);
 

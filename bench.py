@@ -151,6 +151,7 @@ class Workload:
         self.bytes_per_launch = ALGO_BYTES_PER_QUERY * self.n
         self.kernel_events = []  # (start, stop) of every probe launch
         self.served = self.n
+        self.routing = None
         self.config = {"workload": f"probe: {queries // 1_000_000}M x 16B queries vs {PROBE_TABLES} device-resident "
                                    f"filters of {per // 1_000_000}M keys (50% inserted keys)",
                        "queries_total": queries, "queries_this_gpu": self.n, "filters_total": PROBE_TABLES,
@@ -179,7 +180,13 @@ class Workload:
                 return self._probe_local(self.keys, self.fid)
             from adlbloom import dist as D
 
-            out, self.served = D.route_probe(self.keys, self.fid, self.owner, self.local_id, self._probe_local)
+            st = {}
+            out, self.served = D.route_probe(self.keys, self.fid, self.owner, self.local_id, self._probe_local,
+                                             stats=st)
+            # DESIGN.md §6's cost model: (N-1)/N of the queries cross xGMI, 20 B out and 1 B back
+            self.routing = dict(st, bytes_per_query_out=D.ROUTE_BYTES_OUT, bytes_per_query_back=D.ROUTE_BYTES_BACK,
+                                offrank_fraction=round(st["queries_sent_offrank"] / max(self.n, 1), 4),
+                                model_offrank_fraction=round((self.world - 1) / self.world, 4))
             return out
         if self.kind == "varlen":
             return self.builder.build(self.keys, self.offs)
@@ -314,6 +321,15 @@ def probe_check(w, out, rank, world):
         sha = hashlib.sha256(allout.cpu().numpy().tobytes()).hexdigest()
         rec["oracle"] = ("all %dM answers bit-identical to the oracle (sha256)" % (w.total_queries // 1_000_000)
                          if sha == pins["probe"]["results_sha256"] else f"MISMATCH sha256 {sha}")
+    else:  # no pin for this batch: rank 0's first 200K queries to its own filters against the oracle
+        fid0 = w.fid.cpu().numpy().astype(np.int64)
+        sel0 = np.nonzero((fid0 >= w.tables.start) & (fid0 < w.tables.stop))[0][:200_000]
+        want = O.probe_multi(w.keys.cpu().numpy()[sel0], (fid0[sel0] - w.tables.start).astype(np.uint32),
+                             w.bitmaps.cpu().numpy(), np.asarray(w.bitmap_off_host, dtype=np.uint64),
+                             bits_per_key=BPK)
+        got = out.cpu().numpy()[sel0]
+        rec["oracle"] = ("parity unpinned (no pin for this batch); %d sampled answers identical to the oracle"
+                         % sel0.size if np.array_equal(got, want) else "MISMATCH on sampled answers")
     # reads per query on rank 0's own filters
     fid_all = w.fid.cpu().numpy().astype(np.int64)
     sel = np.nonzero((fid_all >= w.tables.start) & (fid_all < w.tables.stop))[0][:200_000]
@@ -337,17 +353,26 @@ def probe_check(w, out, rank, world):
 
 def build_parity(w, rank):
     """Rank 0's bitmaps against the oracle pins (varlen, compaction)."""
-    pins = load_pins()
-    if rank != 0 or not pins:
+    pins = load_pins() or {"varlen": {"n": -1}, "compaction": {"bitmap_sha256": {}}}
+    if rank != 0:
         return None
     if w.kind == "varlen":
         p = pins["varlen"]
         if w.n != p["n"]:
-            return None
+            return oracle_build_check(w.builder.bitmap[:w.builder.nbytes], w.keys, w.offs, w.n)
         sha = hashlib.sha256(w.builder.bitmap[:w.builder.nbytes].cpu().numpy().tobytes()).hexdigest()
         return "bit-identical to the oracle (sha256)" if sha == p["bitmap_sha256"] else f"MISMATCH sha256 {sha}"
     if w.kind == "compaction":
         want = pins["compaction"]["bitmap_sha256"]
+        if isinstance(want, dict) or len(want) != COMPACTION_TABLES:  # no pins: two tables against the oracle
+            sys.path.insert(0, os.path.join(ROOT, "oracle"))
+            import oracle as O
+
+            bad = [t for i, t in list(enumerate(w.tables))[:2]
+                   if not np.array_equal(w.builder.bitmap(i).cpu().numpy(),
+                                         O.keys2block(O.splitmix_keys16(0x5EED + t, 1_000_000), bits_per_key=BPK))]
+            return ("parity unpinned (no pins): 2 tables bit-identical to the oracle" if not bad
+                    else f"MISMATCH tables {bad}")
         bad = [t for i, t in enumerate(w.tables)
                if hashlib.sha256(w.builder.bitmap(i).cpu().numpy().tobytes()).hexdigest() != want[t]]
         return (f"all {len(w.tables)} bitmaps of this GPU bit-identical to the oracle (sha256)" if not bad
@@ -487,28 +512,81 @@ def e2e_compaction(w, iters=3):
             "unpipelined": {"value": round(n / ds / 1e6, 1), "ms_per_build": round(ds * 1e3, 3)}}
 
 
-def parity_check(bm_dev, n):
-    """Rank-0 bitmap vs the reference's SHA-256 for the seed-0x5EED key set."""
+def parity_check(bm_dev, n, keys=None):
+    """Rank-0 bitmap vs the reference's SHA-256 for the seed-0x5EED key set; for
+    a size the pins do not cover, against the oracle's build of the same keys
+    (up to 20M keys), else a sampled statement."""
     path = os.path.join(ROOT, "tests", "golden", "appendix_b.json")
     try:
         gold = {g["n"]: g["sha256"] for g in json.load(open(path))["bitmaps"]}
-    except OSError:
-        return None
-    if n not in gold:
-        return None
-    sha = hashlib.sha256(bm_dev.cpu().numpy().tobytes()).hexdigest()
-    return "bit-identical to reference (sha256)" if sha == gold[n] else f"MISMATCH sha256 {sha}"
+    except (OSError, ValueError):
+        gold = {}
+    if n in gold:
+        sha = hashlib.sha256(bm_dev.cpu().numpy().tobytes()).hexdigest()
+        return "bit-identical to reference (sha256)" if sha == gold[n] else f"MISMATCH sha256 {sha}"
+    return oracle_build_check(bm_dev, keys, None, n)
+
+
+def oracle_build_check(bm_dev, keys, offs, n):
+    """Parity of a build the pins do not cover: the oracle's bitmap of the same
+    keys (n <= 20M: a few seconds of CPU), or -- larger -- 'parity unpinned'
+    with a sampled check that every bit of 100K of the keys is set."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+
+    got = bm_dev.cpu().numpy()
+    hk = keys.cpu().numpy()
+    ho = offs.cpu().numpy().view(np.uint64) if offs is not None else None
+    if n <= 20_000_000:
+        want = O.keys2block(hk, offsets=ho, bits_per_key=BPK)
+        return ("bit-identical to the oracle (full build of the same keys)" if np.array_equal(got, want)
+                else f"MISMATCH vs the oracle ({int((got != want).sum())} bytes differ)")
+    idx = np.random.default_rng(1).choice(n, 100_000, replace=False)
+    if ho is None:
+        ok = O.probe(hk[idx], got, bits_per_key=BPK).all()
+    else:
+        ks = [hk[int(ho[i]):int(ho[i + 1])].tobytes() for i in idx]
+        ok = O.probe(ks, got, bits_per_key=BPK).all()
+    return ("parity unpinned (no pin for this size); sampled: every bit of 100K keys set" if ok
+            else "MISMATCH: a sampled key has a clear bit")
+
+
+def load_pmc(workload):
+    """This workload's entry of the committed rocprofv3 PMC summary
+    (profiles/pmc_traffic.json, tools/pmc_traffic.py), or {}."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        return json.load(open(path)).get(workload) or {}
+    except (OSError, ValueError):
+        return {}
 
 
 def load_traffic(workload, bytes_per_launch):
     """HBM bytes per build from the committed rocprofv3 PMC summary (profiles/), or None."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    try:
-        d = json.load(open(path))
-    except (OSError, ValueError):
+    return load_pmc(workload).get("hbm_bytes_per_build")
+
+
+# Integer issue ceiling (MI355X_MICROARCH.md): 256 CUs x 4 SIMDs, one wave64
+# VALU instruction per SIMD every 2 cycles, at the clock the PMC pass measured
+# (GRBM_GUI_ACTIVE / 8 XCDs / kernel time).
+def alu_roofline(workload, n_keys, kernels_us):
+    """roofline.alu (SURVEY.md §8(d)'s secondary bound) from the committed PMC
+    pass: VALU wave-instructions per key of each pass, and the fraction of the
+    integer issue ceiling they take at this run's kernel times."""
+    e = load_pmc(workload).get("alu")
+    if not e:
         return None
-    e = d.get(workload)
-    return None if e is None else e.get("hbm_bytes_per_build")
+    out = {"source": "profiles/pmc_traffic.json (SQ_INSTS_VALU, GRBM_GUI_ACTIVE per kernel)",
+           "issue_model": "256 CUs x 4 SIMDs x 1 wave64 VALU instruction / 2 cycles"}
+    for k, v in e.items():
+        us = kernels_us.get(k)
+        clk = v.get("clock_ghz") or 2.4
+        ceiling = 256 * 4 / 2 * clk * 1e9  # wave-instructions / s
+        out[k] = {"valu_wave_insts": v["valu_wave_insts"],
+                  "valu_lane_ops_per_key": round(v["valu_wave_insts"] * 64 / n_keys, 1),
+                  "clock_ghz": clk,
+                  "issue_frac": round(v["valu_wave_insts"] / (us * 1e-6) / ceiling, 4) if us else None}
+    return out
 
 
 def main():
@@ -575,7 +653,7 @@ def main():
 
     parity = None
     if rank == 0 and args.workload == "single":
-        parity = parity_check(out, w.n)
+        parity = parity_check(out, w.n, w.keys)
     elif probe:
         parity = probe_check(w, out, rank, world)
     else:
@@ -664,6 +742,15 @@ def main():
             }
         if traffic and timed:
             out_json["roofline"]["traffic_gbs"] = round(traffic / (kern_ms * 1e-3) / 1e9, 1)
+        if not probe:
+            out_json["roofline"]["alu"] = alu_roofline(args.workload, w.n, kernels)
+            pos = w.builder.positions()
+            out_json["roofline"]["positions_per_build"] = {
+                "positions": pos, "per_key": round(pos / w.n, 3),
+                "round_trip_bytes": 8 * pos,  # 4 B written by pass A, read by pass B
+                "note": "k bit-sets per key, less the keys whose hash pair their workgroup had already counted"}
+        if probe and world > 1:
+            out_json["roofline"]["routing"] = w.routing
         if world == 1 and args.workload == "single" and not args.no_e2e:
             out_json["e2e"] = e2e(w.n)
         if world == 1 and args.workload == "compaction" and not args.no_e2e:

@@ -83,12 +83,18 @@ uint64_t adl_bloom_build_workspace_bytes(const uint64_t *key_counts, uint32_t nu
  * Replaces BloomFilter::Keys2Block (src/filter_block.cpp:9-33) for a batch.
  *   d_bitmap: adl_bloom_bitmap_alloc_bytes(n, bpk) bytes, 16-byte aligned;
  *             every byte is written (no pre-zeroing needed).
- *   d_workspace: adl_bloom_build_workspace_bytes(&n, 1, bpk) bytes, 256-B aligned. */
+ *   d_workspace: adl_bloom_build_workspace_bytes(&n, 1, bpk) bytes, 256-B aligned.
+ *   d_keys: no alignment or padding is required.  When it is 16-byte aligned
+ *   the kernels may load whole aligned 16-byte blocks that hold key bytes, so
+ *   up to 15 bytes past the last key's end are read (never a block that holds
+ *   no key byte, so never a page the keys do not touch); when it is not, every
+ *   access stays inside the key bytes. */
 int adl_bloom_build_device(const uint8_t *d_keys, const uint64_t *d_offsets, uint64_t n,
                            uint32_t key_stride, int32_t bits_per_key, uint8_t *d_bitmap,
                            void *d_workspace, uint64_t workspace_bytes, void *stream);
 
-/* Build num_filters independent filters (one per SSTable) in one pass pair.
+/* Build num_filters independent filters (one per SSTable) in one pass pair
+ * (split only past 2^31 / k keys, where u32 position indices would overflow).
  * Filter f owns keys [key_begin[f], key_begin[f+1]) of the key set and writes
  * its bitmap at d_bitmaps + bitmap_off[f] (16-byte aligned, room for
  * adl_bloom_bitmap_alloc_bytes(n_f, bpk)).  key_begin (num_filters+1 entries)
@@ -121,8 +127,8 @@ int adl_bloom_build(const uint8_t *h_keys, const uint64_t *h_offsets, uint64_t n
 
 /* Host-pointer segmented build for many filters (the compaction shape: one
  * filter per SSTable, keys and bitmaps in host memory), pipelined: filters go
- * in groups (<= 8 filters, ~32 MB of keys) whose key upload, build (on
- * `stream`) and bitmap download overlap on three streams.  Filter f's bitmap,
+ * in groups (~128 MB of keys, one launch pair each) whose key upload, build
+ * (on `stream`) and bitmap download overlap on three streams.  Filter f's bitmap,
  * exactly adl_bloom_bitmap_bytes(n_f, bpk) bytes, is written at
  * h_bitmaps + h_bitmap_off[f] (any alignment, e.g. packed back to back as in
  * a filter block).  Pinned (hipHostMalloc'd / registered) buffers are DMAed
@@ -310,6 +316,13 @@ int adl_bloom_profile_collect(double *ms, uint32_t *builds);
  * pass A and ms_ab[2i+1] = pass B of pair i, for up to `capacity` pairs (for
  * medians); call before adl_bloom_profile_collect. */
 int adl_bloom_profile_each(double *ms_ab, uint32_t capacity, uint32_t *launch_pairs);
+
+/* Bit-sets a build wrote as positions (pass A's output, after it skipped
+ * repeated hash pairs), read back from the workspace of the last build made
+ * with these key counts: *positions = the sum over its chunks.  For the
+ * bench's traffic accounting (profiles/).  Synchronous on `stream`. */
+int adl_bloom_build_positions(const uint64_t *key_counts, uint32_t num_filters, int32_t bits_per_key,
+                              const void *d_workspace, uint64_t *positions, void *stream);
 
 /* Test-only fault injection (the error-path tests; never set by the product).
  * ADL_TEST_FAULT_PIPELINE_GROUP, arg g >= 0: the next adl_bloom_build_segmented
