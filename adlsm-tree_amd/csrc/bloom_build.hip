@@ -185,7 +185,7 @@ __global__ __launch_bounds__(256) void fill_maps_kernel(const FilterDesc *__rest
 // adl_bloom_debug_stamps() (tools/stamps.py).  The product library has none
 // of this.
 #ifdef ADL_BLOOM_STAMPS
-__device__ uint64_t g_stamps[2][2048][8];
+__device__ uint64_t g_stamps[3][2048][8];  // pass A, pass B, hashing pass
 #define STAMP_DECL                                  \
   uint64_t st_acc_[8] = {0, 0, 0, 0, 0, 0, 0, 0}; \
   uint64_t st_t_ = __builtin_amdgcn_s_memtime();
@@ -546,7 +546,7 @@ constexpr uint32_t hv_stage_bytes() {
 
 template <uint32_t S>
 constexpr size_t hv_lds_bytes() {
-  return kHvBins * 4 + S * 4 + S * 2 + hv_stage_bytes<S>() + 16;
+  return kHvBins * 4 + S * 4 + S * 2 + hv_stage_bytes<S>() + 16;  // + hash_lds's read slack
 }
 
 template <uint32_t S, bool DT>
@@ -562,6 +562,7 @@ __global__ __launch_bounds__(kHvBlock) void hash_var_kernel(BuildArgs a, KeysVar
   const int tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid / kWave;
   const uint32_t sc = blockIdx.x;
   if (sc >= total_sc) return;
+  STAMP_DECL
   const auto &d = Filt<DT>::at(a, ft, Filt<DT>::of_run(a, ft, sc));
   const uint32_t first = (sc - d.sc_base) * S;
   const uint32_t cnt = min(S, d.n - first);
@@ -595,6 +596,7 @@ __global__ __launch_bounds__(kHvBlock) void hash_var_kernel(BuildArgs a, KeysVar
     for (int i = 0; i < VPT; ++i) v[i] = src[min((uint32_t)(tid + i * kHvBlock), nv - 1u)];
   }
   __syncthreads();
+  STAMP(0);  // offsets and key bytes loaded
   // ---- sort the run's keys by length
   uint32_t rk[KPT];
 #pragma unroll
@@ -612,6 +614,7 @@ __global__ __launch_bounds__(kHvBlock) void hash_var_kernel(BuildArgs a, KeysVar
       if (tid + i * kHvBlock < nv) dst[tid + i * kHvBlock] = v[i];
   }
   __syncthreads();
+  STAMP(1);  // lengths counted, bytes staged
   if (wave == 0) {  // exclusive scan of the bins, 8 per lane
     constexpr int PER = kHvBins / kWave;
     uint32_t bv[PER], t = 0;
@@ -622,6 +625,7 @@ __global__ __launch_bounds__(kHvBlock) void hash_var_kernel(BuildArgs a, KeysVar
     for (int j = 0; j < PER; ++j) bins[lane * PER + j] = run, run += bv[j];
   }
   __syncthreads();
+  STAMP(2);  // bins scanned
 #pragma unroll
   for (int i = 0; i < KPT; ++i) {
     if (rk[i] != ~0u) {
@@ -636,12 +640,15 @@ __global__ __launch_bounds__(kHvBlock) void hash_var_kernel(BuildArgs a, KeysVar
     }
   }
   __syncthreads();
+  STAMP(3);  // slots scattered
 
   // ---- hash, group g = 64 sorted slots
   const uint32_t groups = (cnt + kWave - 1) / kWave;
   uint2 *out = hp + (uint64_t)d.chunk_base * a.C + first;
   // longest groups first (slots are sorted by length): the waves start on the
-  // groups that set the workgroup's end, and the short ones fill in behind
+  // groups that set the workgroup's end, and the short ones fill in behind.
+  // (A queue handing each free wave the next group measured the same: the
+  // longest group alone sets the end.)
   for (uint32_t gi = wave; gi < groups; gi += NW) {
     const uint32_t g = groups - 1 - gi;
     const uint32_t s = g * kWave + lane;
@@ -649,6 +656,12 @@ __global__ __launch_bounds__(kHvBlock) void hash_var_kernel(BuildArgs a, KeysVar
     uint32_t len = s_len[s];
     const uint32_t r = s_rel[s];
     uint32_t h1, h2;
+#ifdef ADL_BLOOM_STAMPS
+    if (a.exp & 16) {  // diagnostics: no hashing (wrong pairs)
+      out[s] = make_uint2(r, len | 1u);
+      continue;
+    }
+#endif
     if (len < 0xffffu && (uint64_t)r + len <= sbytes) {
       hash_lds(stage, r, len, h1, h2);
     } else {
@@ -661,6 +674,8 @@ __global__ __launch_bounds__(kHvBlock) void hash_var_kernel(BuildArgs a, KeysVar
     }
     out[s] = make_uint2(h1, h2);
   }
+  STAMP(4);  // this wave's groups hashed and stored
+  STAMP_FLUSH(2);
 }
 
 // Key sources of bloom_bin16_kernel: raw 16-byte keys (hashed in pass A), or
@@ -1552,7 +1567,7 @@ int adl_bloom_test_fault(int site, int64_t arg) {
 #ifdef ADL_BLOOM_STAMPS
 // Diagnostics build only: copies g_stamps ([pass][workgroup][phase] cycles).
 int adl_bloom_debug_stamps(uint64_t *out, uint64_t n) {
-  const uint64_t bytes = std::min<uint64_t>(n, 2 * 2048 * 8) * 8;
+  const uint64_t bytes = std::min<uint64_t>(n, 3 * 2048 * 8) * 8;
   ADL_HIP_TRY(hipDeviceSynchronize());
   ADL_HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), bytes, 0, hipMemcpyDeviceToHost));
   return ADL_OK;

@@ -37,13 +37,20 @@ __device__ __forceinline__ uint32_t rotl_quirk(uint32_t x) {
   return (x << C) | (uint32_t)((int32_t)x >> (32 - C));
 }
 
-__device__ __forceinline__ uint32_t mix_block(uint32_t h, uint32_t k) {
+// The block word's own mixing (src/murmur3_hash.cpp:31-33).  It does not
+// depend on the seed, so the two hashes of a key share it: two quarter-rate
+// v_mul_lo_u32 per block instead of four.
+__device__ __forceinline__ uint32_t mix_k(uint32_t k) {
   k *= 0xcc9e2d51u;       // :31
   // opaque: otherwise the compiler folds the rotate's k << 15 into a second
   // v_mul_lo_u32 by c1 << 15 (a quarter-rate op for a full-rate shift)
   asm("" : "+v"(k));
   k = rotl_quirk<15>(k);  // :32
-  k *= 0x1b873593u;       // :33
+  return k * 0x1b873593u; // :33
+}
+
+// The state update with a mixed block word (src/murmur3_hash.cpp:35-37).
+__device__ __forceinline__ uint32_t mix_h(uint32_t h, uint32_t k) {
   h ^= k;                 // :35
   // :36, h*5 + c as shift + 3-input add: an opaque shift keeps the compiler
   // from fusing it back into a 64-bit v_mad_u64_u32
@@ -53,12 +60,20 @@ __device__ __forceinline__ uint32_t mix_block(uint32_t h, uint32_t k) {
   return r4 + r + 0xe6546b64u;
 }
 
-__device__ __forceinline__ uint32_t mix_tail(uint32_t h, uint32_t k1) {
-  k1 *= 0xcc9e2d51u;  // :50-53
-  k1 = rotl_quirk<15>(k1);
-  k1 *= 0x1b873593u;
-  return h ^ k1;
+__device__ __forceinline__ uint32_t mix_block(uint32_t h, uint32_t k) { return mix_h(h, mix_k(k)); }
+
+// Both seeds' states advanced by one block word.
+__device__ __forceinline__ void mix_block2(uint32_t &a, uint32_t &b, uint32_t k) {
+  const uint32_t kk = mix_k(k);
+  a = mix_h(a, kk);
+  b = mix_h(b, kk);
 }
+
+// The tail word mixed (src/murmur3_hash.cpp:50-53), also seed-independent;
+// the state update is h ^= it.
+__device__ __forceinline__ uint32_t mix_tail_k(uint32_t k1) { return mix_k(k1); }
+
+__device__ __forceinline__ uint32_t mix_tail(uint32_t h, uint32_t k1) { return h ^ mix_tail_k(k1); }
 
 __device__ __forceinline__ uint32_t fmix(uint32_t h, uint32_t len) {
   h ^= len;  // :57-62
@@ -87,10 +102,10 @@ __device__ __forceinline__ void hash16(uint4 raw, uint32_t &h1, uint32_t &h2) {
   const uint32_t w0 = quirk_word(raw.x), w1 = quirk_word(raw.y);
   const uint32_t w2 = quirk_word(raw.z), w3 = quirk_word(raw.w);
   uint32_t a = kSeed1, b = kSeed2;
-  a = mix_block(a, w0); b = mix_block(b, w0);
-  a = mix_block(a, w1); b = mix_block(b, w1);
-  a = mix_block(a, w2); b = mix_block(b, w2);
-  a = mix_block(a, w3); b = mix_block(b, w3);
+  mix_block2(a, b, w0);
+  mix_block2(a, b, w1);
+  mix_block2(a, b, w2);
+  mix_block2(a, b, w3);
   h1 = fmix(a, 16u);
   h2 = fmix(b, 16u);
 }
@@ -116,11 +131,7 @@ __device__ __forceinline__ void hash_bytes(const uint8_t *p, uint32_t len, uint3
     for (uint32_t u = 0; u < U; ++u) w[u] = i + u < nblk ? load_u32_unaligned(p + 4 * (i + u)) : 0u;
 #pragma unroll
     for (uint32_t u = 0; u < U; ++u) {
-      if (i + u < nblk) {
-        const uint32_t q = quirk_word(w[u]);
-        a = mix_block(a, q);
-        b = mix_block(b, q);
-      }
+      if (i + u < nblk) mix_block2(a, b, quirk_word(w[u]));
     }
   }
   const uint32_t rem = len & 3u;
@@ -129,52 +140,57 @@ __device__ __forceinline__ void hash_bytes(const uint8_t *p, uint32_t len, uint3
     uint32_t raw = t[0];
     if (rem >= 2) raw |= (uint32_t)t[1] << 8;
     if (rem >= 3) raw |= (uint32_t)t[2] << 16;
-    const uint32_t k1 = tail_word(raw, rem);
-    a = mix_tail(a, k1);
-    b = mix_tail(b, k1);
+    const uint32_t kk = mix_tail_k(tail_word(raw, rem));
+    a ^= kk;
+    b ^= kk;
   }
   ha = fmix(a, len);
   hb = fmix(b, len);
 }
 
 // Both seeds of a key staged in LDS at byte offset `off` of `stage` (any
-// alignment): one aligned ds_read_b32 per block plus v_alignbyte_b32 with the
-// previous word.  Reads up to 4 bytes past the key's end (callers keep slack).
+// alignment; `stage` 8-byte aligned): aligned LDS words plus v_alignbyte_b32
+// with the previous word.  Reads up to 8 bytes past the key's end (callers
+// keep slack).
 __device__ __forceinline__ void hash_lds(const uint32_t *stage, uint32_t off, uint32_t len,
                                          uint32_t &ha, uint32_t &hb) {
   uint32_t a = kSeed1, b = kSeed2;
   const uint32_t nblk = len >> 2, sh = off & 3u;
   uint32_t wi = off >> 2;
-  uint32_t lo = stage[wi];
   uint32_t i = 0;
-  // four blocks per step: their four LDS words are read before the first is
-  // mixed, so one LDS round trip covers 16 key bytes
+  // Four blocks per step from two 8-byte-aligned ds_read_b64 (the lanes of a
+  // wave read keys at scattered offsets, so every LDS access is a random-bank
+  // one: half the instructions of four ds_read_b32, at about the same cycles
+  // each).  The step's four words are the dword after the carry and the three
+  // after that; a key starting in the high dword of its pair takes them one
+  // dword later (odd), selected per lane.
+  const uint2 *s2 = reinterpret_cast<const uint2 *>(stage);
+  const bool odd = (wi & 1u) != 0;
+  uint2 p0 = s2[wi >> 1];
+  uint32_t lo = odd ? p0.y : p0.x;
+  uint32_t pi = wi >> 1;
   for (; i + 4 <= nblk; i += 4) {
-    uint32_t w[4];
+    const uint2 p1 = s2[pi + 1], p2 = s2[pi + 2];
+    const uint32_t w[4] = {odd ? p1.x : p0.y, odd ? p1.y : p1.x, odd ? p2.x : p1.y, odd ? p2.y : p2.x};
 #pragma unroll
-    for (int u = 0; u < 4; ++u) w[u] = stage[wi + 1 + u];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const uint32_t q = quirk_word(__builtin_amdgcn_alignbyte(w[u], u ? w[u - 1] : lo, sh));
-      a = mix_block(a, q);
-      b = mix_block(b, q);
-    }
+    for (int u = 0; u < 4; ++u)
+      mix_block2(a, b, quirk_word(__builtin_amdgcn_alignbyte(w[u], u ? w[u - 1] : lo, sh)));
     lo = w[3];
+    p0 = p2;
+    pi += 2;
     wi += 4;
   }
   for (; i < nblk; ++i) {
     const uint32_t hi = stage[++wi];
-    const uint32_t q = quirk_word(__builtin_amdgcn_alignbyte(hi, lo, sh));
-    a = mix_block(a, q);
-    b = mix_block(b, q);
+    mix_block2(a, b, quirk_word(__builtin_amdgcn_alignbyte(hi, lo, sh)));
     lo = hi;
   }
   const uint32_t rem = len & 3u;
   if (rem) {
     const uint32_t raw = __builtin_amdgcn_alignbyte(stage[wi + 1], lo, sh);
-    const uint32_t k1 = tail_word(raw, rem);
-    a = mix_tail(a, k1);
-    b = mix_tail(b, k1);
+    const uint32_t kk = mix_tail_k(tail_word(raw, rem));
+    a ^= kk;
+    b ^= kk;
   }
   ha = fmix(a, len);
   hb = fmix(b, len);

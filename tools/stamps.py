@@ -22,6 +22,7 @@ import adlbloom  # noqa: E402
 NAMES = {
     0: ["loop-top (clear, hash)", "count+store(prev)", "scan", "table", "scatter", "epilogue", "-", "-"],
     1: ["tile start", "stage segs", "gather+or", "write+zero tile", "-", "-", "-", "-"],
+    2: ["loads landed", "count + stage", "scan bins", "scatter slots", "hash + store (wave 0)", "-", "-", "-"],
 }
 # the generic pass A (bloom_bin_kernel: variable-length keys, WORKLOAD=varlen)
 NAMES_GENERIC = ["length sort", "hash setup / rest", "count", "scan+table", "scatter", "store", "window load",
@@ -44,12 +45,12 @@ def main():
     L = adlbloom.lib()
     L.adl_bloom_debug_stamps.restype = ctypes.c_int
     L.adl_bloom_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
-    buf = np.zeros((2, 2048, 8), dtype=np.uint64)
+    buf = np.zeros((3, 2048, 8), dtype=np.uint64)
     assert L.adl_bloom_debug_stamps(buf.ctypes.data, buf.size) == 0
-    for p in (0, 1):
+    for p in ((0, 1, 2) if varlen else (0, 1)):
         rows = buf[p][buf[p].sum(axis=1) > 0]
         tot = rows.sum(axis=1).mean()
-        print(f"pass {'AB'[p]}: {len(rows)} workgroups, mean total {tot:.0f} cycles")
+        print(f"pass {'ABH'[p]}: {len(rows)} workgroups, mean total {tot:.0f} cycles")
         for i in range(8):
             if NAMES[p][i] == "-":
                 continue
