@@ -380,6 +380,13 @@ int lds_limit() {
   return ADL_OK;
 }
 
+// Library-internal (bloom_probe.hip): adl_bloom_probe_ranges_device whose
+// kernel launch also completes `done`.
+__attribute__((visibility("hidden"))) int adl_probe_ranges_device_ev(
+    const uint8_t *d_keys, const uint64_t *d_offsets, uint64_t n, uint32_t key_stride, const uint32_t *d_filter_id,
+    uint32_t num_filters, const uint8_t *d_bitmaps, const uint64_t *d_begin, const uint64_t *d_end,
+    int32_t bits_per_key, uint8_t *d_out, hipStream_t st, hipEvent_t done);
+
 // adl_bloom_test_fault's armed sites (-1: off).  take() disarms and returns the
 // argument, so an armed fault fires once.
 struct TestFaults {

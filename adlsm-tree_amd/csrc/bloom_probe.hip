@@ -7,6 +7,7 @@
 // load is coalesced, the k bitmap reads are random byte loads that stop at the
 // first clear bit (the same early exit as the reference), issued a few at a
 // time so that independent reads overlap.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -293,20 +294,35 @@ namespace {
 int probe_multi(const uint8_t *d_keys, const uint64_t *d_offsets, uint64_t n, uint32_t key_stride,
                 const uint32_t *d_filter_id, uint32_t uniform_f, uint32_t num_filters,
                 const uint8_t *d_bitmaps, const uint64_t *d_bitmap_off, int32_t bits_per_key,
-                uint8_t *d_out, hipStream_t st, const uint64_t *d_bitmap_end = nullptr) {
+                uint8_t *d_out, hipStream_t st, const uint64_t *d_bitmap_end = nullptr,
+                hipEvent_t done = nullptr) {
   if (num_filters && (!d_bitmaps || !d_bitmap_off)) return ADL_ERR_INVALID_ARG;
   if (!d_offsets && key_stride == 0) return ADL_ERR_INVALID_ARG;
   const uint32_t k = (uint32_t)adl_host::num_probes(bits_per_key);
   return dispatch_keys(d_keys, d_offsets, key_stride, [&](auto keys) -> int {
     const size_t lds = num_filters <= kLdsFilters ? (size_t)num_filters * sizeof(ModLds) : 0;
-    hipLaunchKernelGGL(bloom_probe_multi_kernel<decltype(keys)>, dim3(grid_for(n, kBlockP, 8)),
-                       dim3(kBlockP), lds, st, keys, n, k, probe_groups(), d_filter_id, uniform_f, num_filters,
-                       d_bitmaps, d_bitmap_off, d_bitmap_end, d_out);
+    // `done` rides on the dispatch packet itself (no marker packet after it)
+    hipExtLaunchKernelGGL(bloom_probe_multi_kernel<decltype(keys)>, dim3(grid_for(n, kBlockP, 8)),
+                          dim3(kBlockP), lds, st, nullptr, done, 0, keys, n, k, probe_groups(), d_filter_id,
+                          uniform_f, num_filters, d_bitmaps, d_bitmap_off, d_bitmap_end, d_out);
     ADL_HIP_TRY(hipGetLastError());
     return ADL_OK;
   });
 }
 }  // namespace
+
+// adl_bloom_probe_ranges_device whose launch also completes `done` (the
+// filter cache's small batches wait on it; see filter_cache.hip).
+int adl_host::adl_probe_ranges_device_ev(const uint8_t *d_keys, const uint64_t *d_offsets, uint64_t n, uint32_t key_stride,
+                               const uint32_t *d_filter_id, uint32_t num_filters, const uint8_t *d_bitmaps,
+                               const uint64_t *d_begin, const uint64_t *d_end, int32_t bits_per_key, uint8_t *d_out,
+                               hipStream_t st, hipEvent_t done) {
+  if (n == 0) return ADL_OK;
+  if (!d_keys || !d_filter_id || !d_out || bits_per_key < 0) return ADL_ERR_INVALID_ARG;
+  if (num_filters && !d_end) return ADL_ERR_INVALID_ARG;
+  return probe_multi(d_keys, d_offsets, n, key_stride, d_filter_id, 0, num_filters, d_bitmaps, d_begin,
+                     bits_per_key, d_out, st, d_end, done);
+}
 
 extern "C" int adl_bloom_probe_ranges_device(const uint8_t *d_keys, const uint64_t *d_offsets, uint64_t n,
                                              uint32_t key_stride, const uint32_t *d_filter_id,

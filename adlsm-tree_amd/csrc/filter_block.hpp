@@ -42,6 +42,11 @@ class KeyArena {
     bytes_.append(key.data(), key.size());
     offsets_.push_back(bytes_.size());
   }
+  /* room for `keys` more keys of `bytes` bytes in all (no reallocation while they are added) */
+  void Reserve(size_t keys, size_t bytes) {
+    bytes_.reserve(bytes_.size() + bytes);
+    offsets_.reserve(offsets_.size() + keys);
+  }
   void Clear() {
     bytes_.clear();
     offsets_.assign(1, 0);

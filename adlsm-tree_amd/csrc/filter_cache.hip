@@ -365,17 +365,17 @@ int adl_bloom_filter_cache_probe(adl_bloom_filter_cache *c, const char *const *o
       if (hbuf == sg.host && hipMemcpyAsync(dbuf, hbuf, o_out, hipMemcpyHostToDevice, st) != hipSuccess)
         rc = ADL_ERR_DEVICE;
     }
+    // a watched batch's completion event rides on the probe's dispatch packet
+    hipEvent_t done = spin && rc == ADL_OK ? t_done.get() : nullptr;
     if (rc == ADL_OK) {
       const uint64_t *d_be = reinterpret_cast<const uint64_t *>(dbuf + o_be);
-      rc = adl_bloom_probe_ranges_device(dbuf, h_offsets ? reinterpret_cast<uint64_t *>(dbuf + o_offs) : nullptr,
-                                         n, key_stride, reinterpret_cast<const uint32_t *>(dbuf + o_fid),
-                                         num_tables, c->arena, d_be, d_be + num_tables, c->bpk, dbuf + o_out, st);
+      rc = adl_host::adl_probe_ranges_device_ev(dbuf, h_offsets ? reinterpret_cast<uint64_t *>(dbuf + o_offs) : nullptr, n,
+                                      key_stride, reinterpret_cast<const uint32_t *>(dbuf + o_fid), num_tables,
+                                      c->arena, d_be, d_be + num_tables, c->bpk, dbuf + o_out, st, done);
     }
     if (rc == ADL_OK && hbuf == sg.host &&
         hipMemcpyAsync(hbuf + o_out, dbuf + o_out, n, hipMemcpyDeviceToHost, st) != hipSuccess)
       rc = ADL_ERR_DEVICE;
-    hipEvent_t done = spin && rc == ADL_OK ? t_done.get() : nullptr;
-    if (done && hipEventRecord(done, st) != hipSuccess) done = nullptr;
     // the kernel and the copies are done before any pinned range can be reused
     bool finished = false;
     if (done) {

@@ -75,25 +75,74 @@ void LevelCandidates(const vector<TableRange> &tables, const vector<string_view>
   std::stable_sort(asc.begin(), asc.end(), [&](uint32_t a, uint32_t b) {
     return InnerKeyLess(tables[a].min_inner_key, tables[b].min_inner_key);
   });
-  // the ranges decoded once (the inner keys outlive this call)
   vector<Decoded> mn(T), mx(T);
   for (size_t t = 0; t < T; ++t) {
     mn[t] = Decode(tables[t].min_inner_key);
     mx[t] = Decode(tables[t].max_inner_key);
   }
-  // Table t is a candidate for lookup mk (src/revision.cpp:281-287) iff
-  //   mn[t].user <= mk.user  (not "mk < mn and the user keys differ") and
-  //   !(mx[t] < mk).
-  // Sweep the lookups in MemKey order: a table enters when the sweep reaches
-  // its min user key -- in ascending min order, at the front of the active
-  // list, which so stays in Level::Get's visiting order -- and leaves for good
-  // once its max is below the lookup.  Each lookup then reads its candidates
-  // off the active list: O((K + T) log(K + T) + candidates) instead of K * T
-  // range tests.
-  vector<uint32_t> order(K);
-  std::iota(order.begin(), order.end(), 0u);
-  std::stable_sort(order.begin(), order.end(),
-                   [&](uint32_t a, uint32_t b) { return user_keys[a].compare(user_keys[b]) < 0; });
+  // Table t is a candidate for lookup mk = (u, seq, OP_PUT) (src/revision.cpp:
+  // 281-287) iff mn[t].user <= u and !(mx[t] < mk): with seq fixed for the
+  // batch, that is u in [mn.user, mx.user), plus u == mx.user unless
+  // gone_at_max[t] = (mx[t] < (mx.user, seq, OP_PUT)).  So the candidate list
+  // is constant on each region the tables' boundary user keys B cut the key
+  // space into (a gap between two of them, or one of them).  One sweep over B
+  // builds every region's list in Level::Get's visiting order -- a table enters
+  // at the front of the active list (ascending min order, so the list stays in
+  // visiting order) and leaves at its max -- and a lookup is a binary search
+  // in B plus a copy: O(K log T + candidates), no K x T range tests.
+  vector<string_view> B;
+  B.reserve(2 * T);
+  for (size_t t = 0; t < T; ++t) {
+    B.push_back(mn[t].user);
+    B.push_back(mx[t].user);
+  }
+  std::sort(B.begin(), B.end());
+  B.erase(std::unique(B.begin(), B.end()), B.end());
+  const size_t NB = B.size();
+  // lookups compare a 16-byte big-endian prefix first (two u64 compares), the
+  // whole keys only on a tie
+  struct Pref {
+    uint64_t hi, lo;
+  };
+  auto pref = [](string_view u) {
+    uint64_t w[2] = {0, 0};
+    memcpy(w, u.data(), u.size() < 16 ? u.size() : 16);
+    return Pref{__builtin_bswap64(w[0]), __builtin_bswap64(w[1])};
+  };
+  vector<Pref> bp(NB);
+  for (size_t i = 0; i < NB; ++i) bp[i] = pref(B[i]);
+  auto less_b = [&](size_t i, const Pref &p, string_view u) {  // B[i] < u
+    if (bp[i].hi != p.hi) return bp[i].hi < p.hi;
+    if (bp[i].lo != p.lo) return bp[i].lo < p.lo;
+    return B[i] < u;
+  };
+  auto at_p = [&](const Pref &p, string_view u) {  // lower_bound
+    size_t lo = 0, n = NB;
+    while (n) {
+      const size_t h = n / 2;
+      if (less_b(lo + h, p, u)) {
+        lo += h + 1;
+        n -= h + 1;
+      } else {
+        n = h;
+      }
+    }
+    return (uint32_t)lo;
+  };
+  auto at = [&](string_view u) { return at_p(pref(u), u); };
+  vector<vector<uint32_t>> ins(NB), out_pt(NB), out_gap(NB);  // per boundary: enter, leave before / after it
+  // a table whose max user key sorts before its min (no real table) is never a candidate
+  vector<uint8_t> never(T, 0);
+  for (size_t t = 0; t < T; ++t) never[t] = mx[t].user < mn[t].user;
+  for (uint32_t t : asc)
+    if (!never[t]) ins[at(mn[t].user)].push_back(t);
+  for (size_t t = 0; t < T; ++t) {
+    if (never[t]) continue;
+    const bool gone_at_max = Less(mx[t], Decoded{mx[t].user, seq, 0});
+    (gone_at_max ? out_pt : out_gap)[at(mx[t].user)].push_back((uint32_t)t);
+  }
+  // region r: 2i = the gap before B[i], 2i+1 = B[i], 2*NB = the gap after the last
+  vector<uint32_t> rbeg(2 * NB + 2, 0), rlist;
   constexpr uint32_t kNil = ~0u;
   vector<uint32_t> nxt(T, kNil), prv(T, kNil);
   uint32_t head = kNil;
@@ -102,38 +151,35 @@ void LevelCandidates(const vector<TableRange> &tables, const vector<string_view>
     else head = nxt[t];
     if (nxt[t] != kNil) prv[nxt[t]] = prv[t];
   };
-  auto mx_after = [&](uint32_t a, uint32_t b) { return Less(mx[b], mx[a]); };  // min-heap on mx
-  vector<uint32_t> heap;
-  vector<uint32_t> cbeg(K + 1, 0), cand;  // candidates by sorted lookup
-  size_t ins = 0;
-  for (size_t r = 0; r < K; ++r) {
-    const Decoded mk{user_keys[order[r]], seq, 0 /* OP_PUT */};
-    for (; ins < T && mn[asc[ins]].user.compare(mk.user) <= 0; ++ins) {
-      const uint32_t t = asc[ins];
+  auto record = [&](size_t r) {
+    for (uint32_t t = head; t != kNil; t = nxt[t]) rlist.push_back(t);
+    rbeg[r + 1] = (uint32_t)rlist.size();
+  };
+  for (size_t i = 0; i < NB; ++i) {
+    record(2 * i);  // the gap before B[i]
+    for (uint32_t t : ins[i]) {
       nxt[t] = head;
       prv[t] = kNil;
       if (head != kNil) prv[head] = t;
       head = t;
-      heap.push_back(t);
-      std::push_heap(heap.begin(), heap.end(), mx_after);
     }
-    while (!heap.empty() && Less(mx[heap.front()], mk)) {
-      unlink(heap.front());
-      std::pop_heap(heap.begin(), heap.end(), mx_after);
-      heap.pop_back();
-    }
-    for (uint32_t t = head; t != kNil; t = nxt[t]) cand.push_back(t);
-    cbeg[r + 1] = (uint32_t)cand.size();
+    for (uint32_t t : out_pt[i]) unlink(t);
+    record(2 * i + 1);
+    for (uint32_t t : out_gap[i]) unlink(t);
   }
-  // back to the caller's key order
-  vector<uint32_t> rank(K);
-  for (size_t r = 0; r < K; ++r) rank[order[r]] = (uint32_t)r;
-  table.reserve(cand.size());
+  record(2 * NB);
+  // each key's region, then the lists copied out in one pass
+  vector<uint32_t> reg(K);
   for (size_t i = 0; i < K; ++i) {
-    const uint32_t r = rank[i];
-    table.insert(table.end(), cand.begin() + cbeg[r], cand.begin() + cbeg[r + 1]);
-    begin[i + 1] = (uint32_t)table.size();
+    const string_view u = user_keys[i];
+    const uint32_t j = at(u);
+    const uint32_t r = (j < NB && B[j] == u) ? 2 * j + 1 : 2 * j;
+    reg[i] = r;
+    begin[i + 1] = begin[i] + (rbeg[r + 1] - rbeg[r]);
   }
+  table.resize(begin[K]);
+  for (size_t i = 0; i < K; ++i)
+    std::copy(rlist.begin() + rbeg[reg[i]], rlist.begin() + rbeg[reg[i] + 1], table.begin() + begin[i]);
 }
 
 RC LevelMultiGetFilter(FilterCache &cache, const vector<TableRange> &tables, const vector<string_view> &user_keys,
@@ -143,6 +189,9 @@ RC LevelMultiGetFilter(FilterCache &cache, const vector<TableRange> &tables, con
   // the probe batch: pair p = (key, table); SSTableReader::Get probes the user
   // key (src/sstable.cpp:238)
   KeyArena batch;
+  size_t bytes = 0;
+  for (size_t i = 0; i < user_keys.size(); ++i) bytes += (size_t)(out.begin[i + 1] - out.begin[i]) * user_keys[i].size();
+  batch.Reserve(out.table.size(), bytes);
   for (size_t i = 0; i < user_keys.size(); ++i)
     for (uint32_t c = out.begin[i]; c < out.begin[i + 1]; ++c) batch.Add(user_keys[i]);
   const size_t T = tables.size();

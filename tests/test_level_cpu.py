@@ -47,7 +47,7 @@ def candidates(f, tables, keys, seq):
     return [list(table[begin[i]:begin[i + 1]]) for i in range(len(keys))]
 
 
-@pytest.mark.parametrize("seed", range(12))
+@pytest.mark.parametrize("seed", range(32))
 def test_level_candidates_vs_oracle(lvl, oracle, seed):
     rng = np.random.default_rng(seed)
     users = sorted({bytes(rng.integers(97, 101, int(rng.integers(1, 4))).astype(np.uint8)) for _ in range(30)})

@@ -1,0 +1,35 @@
+#!/bin/bash
+# tools/r03_final.sh -- round-3 evidence in one GPU call: PMC passes (traffic +
+# integer issue) written into profiles/pmc_traffic.json first (bench.py reads
+# them), the GPU test suite, smoke(), the read-path latency bench, every bench
+# workload with CPU baselines, and rocprofv3 kernel traces of the headline and
+# var-len runs.
+set -u
+cd "$(dirname "$0")/.."
+OUT=gpurun_out/${TAG:-r03f}
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+step() { echo "=== $1 ($(date +%T))"; }
+step pmc
+bash tools/r03_pmc.sh "$OUT/pmc" single varlen compaction probe > "$OUT/pmc.log" 2>&1 || { tail -5 "$OUT/pmc.log"; exit 1; }
+step pytest
+timeout -k 10 900 python -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -n 4 "$OUT/pytest_gpu.log"; [ $rc -ne 0 ] && exit $rc
+step smoke
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > "$OUT/smoke.log" 2>&1 || exit 1
+tail -n 1 "$OUT/smoke.log"
+step readpath
+timeout -k 10 300 adlsm-tree_amd/bin/readpath_test --bench > "$OUT/readpath_bench.json" 2> "$OUT/readpath_bench.err" || exit 1
+step bench_all
+bash tools/bench_all.sh || exit 1
+cp gpurun_out/bench_all.jsonl "$OUT/bench_all.jsonl"
+step rocprof
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
+  python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-e2e > "$OUT/prof_bench.json" 2> "$OUT/prof.err" || exit 1
+step rocprof_varlen
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_varlen" -o run --output-format csv -- \
+  python3 bench.py --steps 20 --warmup 5 --workload varlen --no-cpu-baseline --no-e2e > "$OUT/prof_varlen_bench.json" 2> "$OUT/prof_varlen.err" || exit 1
+step rocprof_probe
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_probe" -o run --output-format csv -- \
+  python3 bench.py --steps 5 --warmup 2 --workload probe --no-cpu-baseline --no-e2e > "$OUT/prof_probe_bench.json" 2> "$OUT/prof_probe.err" || exit 1
+exit 0
