@@ -94,7 +94,7 @@ struct BuildArgs {
   uint32_t dd_mode;    // 1: every key claims its (h1, h2); 2: keys with h1 == h2 claim h1 (ADL_BLOOM_DD_MODE)
   uint32_t var_hash;   // variable-length keys: length-sorted hashing pass + pass A over (h1, h2) (ADL_BLOOM_VAR_HASH)
   uint32_t exp;        // diagnostics build only (ADL_BLOOM_EXP bits, wrong results): pass A 1 no hash,
-                       // 2 no position stores; pass B 4 no ds_or, 8 no bitmap stores
+                       // 2 no position stores, 32 no reduction; pass B 4 no ds_or, 8 no bitmap stores
   FilterDesc f[kMaxFilters];
 };
 
@@ -838,6 +838,11 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin16_kernel(BuildArgs a, Src key
       if ((live >> i) & 1u) {
 #pragma unroll
         for (int j = 0; j < K; ++j) pos[i][j] = fastmod(h1[i] + (uint32_t)j * h2[i], mod);
+#ifdef ADL_BLOOM_STAMPS
+        if (a.exp & 32)  // diagnostics: no reduction (wrong positions, inside m for m >= 2^29)
+#pragma unroll
+          for (int j = 0; j < K; ++j) pos[i][j] = (h1[i] + (uint32_t)j * h2[i]) >> 3;
+#endif
 #pragma unroll
         for (int j = 0; j < K; ++j) atomicAdd(&hist[pos[i][j] >> TL], 1u);
       }

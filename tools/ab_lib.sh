@@ -1,0 +1,15 @@
+#!/bin/bash
+# tools/ab_lib.sh -- interleaved A/B of bench.py over library builds:
+# LIBS="abl/base/libadlbloom.so|adlsm-tree_amd/lib/libadlbloom.so" REPS=3 bash tools/ab_lib.sh
+set -u
+cd "$(dirname "$0")/.."
+mkdir -p gpurun_out
+IFS='|' read -ra VARIANTS <<< "${LIBS}"
+for rep in $(seq 1 ${REPS:-3}); do
+  for v in "${VARIANTS[@]}"; do
+    out=$(ADL_BLOOM_LIB=$v timeout -k 10 300 python3 bench.py --steps ${STEPS:-30} --warmup 5 --no-cpu-baseline --no-e2e ${BENCH_ARGS:-} 2>/dev/null | grep '^{')
+    rc=$?
+    [ $rc -ne 0 ] && { echo "variant '$v' rc=$rc"; exit $rc; }
+    echo "$v :: $(echo "$out" | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"], d["roofline"]["us_per_step"], d["parity"])')"
+  done
+done | tee gpurun_out/ab_lib.log
