@@ -574,6 +574,7 @@ __global__ __launch_bounds__(kHvBlock) void hash_var_kernel(BuildArgs a, KeysVar
   // up to 15 bytes past the run's last key are read, never a block the key
   // bytes do not touch (include/adl_bloom.h)
   constexpr uint32_t kStage = hv_stage_bytes<S>();
+  static_assert(kStage % (16 * kHvBlock) == 0, "the staging loads cover kStage in whole rounds of 16 B per thread");
   const uint32_t sbytes = (uint32_t)min((end - base16 + 15) & ~15ull, (uint64_t)kStage);
 
   // ---- load the run's offsets and key bytes: every load in flight before

@@ -80,8 +80,11 @@ struct Plan {
   uint32_t F = 0, k = 0, C = 0, nb = 0;
   uint64_t maxch = 0;
   // workspace byte offsets
-  uint64_t o_desc, o_scal, o_cnt, o_start, o_cf, o_dest, o_hs, o_ent, o_tab, o_res, total;
+  uint32_t ng = 0;  // groups of kScanGroup blocks (K2)
+  uint64_t o_desc, o_scal, o_cnt, o_start, o_gsum, o_cf, o_dest, o_hs, o_ent, o_tab, o_res, total;
 };
+
+constexpr uint32_t kScanGroup = 64;  // blocks per column-sum group (K2)
 
 Plan make_plan(uint64_t n, uint32_t F, int32_t bpk) {
   Plan p;
@@ -103,6 +106,8 @@ Plan make_plan(uint64_t n, uint32_t F, int32_t bpk) {
   p.o_scal = take(256);
   p.o_cnt = take((uint64_t)(F + 1) * p.nb * 4);
   p.o_start = take((uint64_t)(F + 1) * p.nb * 4);
+  p.ng = (p.nb + kScanGroup - 1) / kScanGroup;
+  p.o_gsum = take((uint64_t)(F + 1) * p.ng * 4);
   p.o_cf = take(p.maxch * 4);
   p.o_dest = take(n * 2);
   p.o_hs = take(n * 8);
@@ -177,6 +182,104 @@ __global__ __launch_bounds__(kBlk) void pb_hist_kernel(const uint32_t *__restric
 }
 
 // ---------------------------------------------------------------- K2
+// Three launches, every access to the block-major counts a whole-row
+// (coalesced) one:
+//   K2a  per group of kScanGroup blocks: each filter's count over the group
+//   K2b  one workgroup: per filter, the groups' exclusive prefix (in place) and
+//        the total; over the filters, query / chunk / table-entry starts; the
+//        chunk -> filter map
+//   K2c  per group: each block's first slot in every filter's run
+__global__ __launch_bounds__(kBlk) void pb_colsum_kernel(const uint32_t *__restrict__ cnt, uint32_t nb, uint32_t F,
+                                                         uint32_t *__restrict__ gsum) {
+  const uint32_t b0 = blockIdx.x * kScanGroup, b1 = min(b0 + kScanGroup, nb);
+  const uint64_t stride = F + 1;
+  for (uint32_t f = threadIdx.x; f <= F; f += kBlk) {
+    uint32_t s = 0;
+    for (uint32_t b = b0; b < b1; ++b) s += cnt[b * stride + f];
+    gsum[(uint64_t)blockIdx.x * stride + f] = s;
+  }
+}
+
+__global__ __launch_bounds__(kBlk) void pb_plan_kernel(uint32_t *__restrict__ gsum, uint32_t ng, uint32_t F,
+                                                       uint32_t C, uint64_t maxch, PFilter *__restrict__ desc,
+                                                       uint32_t *__restrict__ chunk_filter,
+                                                       uint32_t *__restrict__ scal) {
+  __shared__ uint32_t scratch[kBlk / kWave + 1];
+  __shared__ uint64_t red[kBlk / kWave];
+  const uint64_t stride = F + 1;
+  uint64_t cq = 0, cc = 0, ct = 0;  // running query / chunk / table-entry starts over filter blocks
+  for (uint32_t f0 = 0; f0 <= F; f0 += kBlk) {
+    const uint32_t f = f0 + threadIdx.x;
+    uint32_t tot = 0;
+    if (f <= F) {
+      // the column's group sums, 16 loads in flight at a time (a store between
+      // two loads of one array would serialise them)
+      constexpr uint32_t U = 16;
+      for (uint32_t g0 = 0; g0 < ng; g0 += U) {
+        uint32_t v[U];
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u) v[u] = g0 + u < ng ? gsum[(g0 + u) * stride + f] : 0u;
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u) {
+          if (g0 + u < ng) gsum[(g0 + u) * stride + f] = tot;
+          tot += v[u];
+        }
+      }
+    }
+    const uint32_t tiles = f < F ? desc[f].tiles : 0u;
+    const uint32_t nc = f < F ? (tot + C - 1) / C : 0u;  // the out-of-range bucket has no chunks
+    // exclusive prefixes over the filters (64-bit table entries)
+    uint32_t all_q, all_c;
+    const uint32_t pq = block_excl_scan<kBlk>(f <= F ? tot : 0u, scratch, &all_q);
+    const uint32_t pc = block_excl_scan<kBlk>(nc, scratch, &all_c);
+    const uint64_t te = (uint64_t)(tiles + 1) * nc;
+    // 64-bit exclusive scan of the table entries: wave sums, then the waves before
+    const uint32_t lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
+    uint64_t incl = te;
+    for (int o = 1; o < kWave; o <<= 1) {
+      const uint64_t y = __shfl_up(incl, o, kWave);
+      if ((int)lane >= o) incl += y;
+    }
+    if (lane == kWave - 1) red[wave] = incl;
+    __syncthreads();
+    uint64_t before = 0, all_t = 0;
+    for (uint32_t w = 0; w < kBlk / kWave; ++w) {
+      if (w < wave) before += red[w];
+      all_t += red[w];
+    }
+    __syncthreads();
+    if (f <= F) {
+      desc[f].cnt = tot;
+      desc[f].qbase = (uint32_t)(cq + pq);
+      desc[f].chunk_base = (uint32_t)(cc + pc);
+      desc[f].nchunks = nc;
+      desc[f].table_base = ct + before + incl - te;
+      for (uint32_t j = 0; j < nc; ++j) chunk_filter[cc + pc + j] = f;
+      if (f == F) scal[1] = (uint32_t)(cc + pc);  // chunks over all filters
+    }
+    cq += all_q;
+    cc += all_c;
+    ct += all_t;
+  }
+  __syncthreads();
+  for (uint64_t j = cc + threadIdx.x; j < maxch; j += kBlk) chunk_filter[j] = kSentinel;
+}
+
+__global__ __launch_bounds__(kBlk) void pb_starts_kernel(const uint32_t *__restrict__ cnt,
+                                                         const uint32_t *__restrict__ gsum, uint32_t nb, uint32_t F,
+                                                         const PFilter *__restrict__ desc,
+                                                         uint32_t *__restrict__ start) {
+  const uint32_t b0 = blockIdx.x * kScanGroup, b1 = min(b0 + kScanGroup, nb);
+  const uint64_t stride = F + 1;
+  for (uint32_t f = threadIdx.x; f <= F; f += kBlk) {
+    uint32_t run = desc[f].qbase + gsum[(uint64_t)blockIdx.x * stride + f];
+    for (uint32_t b = b0; b < b1; ++b) {
+      start[b * stride + f] = run;
+      run += cnt[b * stride + f];
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void pb_rows_kernel(const uint32_t *__restrict__ hist, uint32_t nb, uint32_t F,
                                                       PFilter *__restrict__ desc) {
   __shared__ uint32_t red[256];
@@ -717,11 +820,21 @@ int adl_bloom_probe_batch_device(const uint8_t *d_keys, const uint64_t *d_offset
     ADL_HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(pb_hist_kernel, dim3(p.nb), dim3(kBlk), lds_k1, st, d_filter_id, n, F, p.nb, desc, cnt);
     ADL_HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(pb_rows_kernel, dim3(F + 1), dim3(256), 0, st, cnt, p.nb, F, desc);
-    ADL_HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(pb_scan_kernel, dim3(F + 1), dim3(kBlk), 0, st, cnt, start, p.nb, F, p.C, p.maxch, desc, cf,
-                       scal);
-    ADL_HIP_TRY(hipGetLastError());
+    if (getenv("ADL_PB_OLDSCAN")) {  // round-2 K2 (tuning A/B)
+      hipLaunchKernelGGL(pb_rows_kernel, dim3(F + 1), dim3(256), 0, st, cnt, p.nb, F, desc);
+      ADL_HIP_TRY(hipGetLastError());
+      hipLaunchKernelGGL(pb_scan_kernel, dim3(F + 1), dim3(kBlk), 0, st, cnt, start, p.nb, F, p.C, p.maxch, desc, cf,
+                         scal);
+      ADL_HIP_TRY(hipGetLastError());
+    } else {
+      uint32_t *gsum = reinterpret_cast<uint32_t *>(ws + p.o_gsum);
+      hipLaunchKernelGGL(pb_colsum_kernel, dim3(p.ng), dim3(kBlk), 0, st, cnt, p.nb, F, gsum);
+      ADL_HIP_TRY(hipGetLastError());
+      hipLaunchKernelGGL(pb_plan_kernel, dim3(1), dim3(kBlk), 0, st, gsum, p.ng, F, p.C, p.maxch, desc, cf, scal);
+      ADL_HIP_TRY(hipGetLastError());
+      hipLaunchKernelGGL(pb_starts_kernel, dim3(p.ng), dim3(kBlk), 0, st, cnt, gsum, p.nb, F, desc, start);
+      ADL_HIP_TRY(hipGetLastError());
+    }
     if (int rc = adl_host::lds_limit<pb_scatter_kernel>()) return rc;
     hipLaunchKernelGGL(pb_scatter_kernel, dim3(p.nb), dim3(kBlk), lds_k3, st, reinterpret_cast<const uint4 *>(d_keys),
                        d_filter_id, n, F, p.nb, desc, cnt, start, dest, hs);
