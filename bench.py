@@ -663,10 +663,10 @@ def main():
         if probe:
             kern_ms = probe_ms
             kernels = {"probe (adl_bloom_probe_batch_device)": round(probe_ms * 1e3, 2)}
-            kname = ("adl_bloom_probe_batch_device: tile-binned pipeline pb_* (7 launches) for large 16-byte "
+            kname = ("adl_bloom_probe_batch_device: tile-binned pipeline pb_* (9 launches) for large 16-byte "
                      "batches, bloom_probe_multi_kernel otherwise")
         else:
-            # kernel time per step (a segmented build is one launch pair per group of 8 filters)
+            # kernel time per step (every filter of a segmented build in one launch pair)
             kern_ms = (ms_a + ms_b) / max(args.steps, 1)
             kernels = {"bloom_bin_kernel": round(ms_a / max(args.steps, 1) * 1e3, 2),
                        "bloom_tile_kernel": round(ms_b / max(args.steps, 1) * 1e3, 2)}

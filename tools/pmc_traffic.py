@@ -21,6 +21,7 @@ from collections import defaultdict
 root, out, workload = sys.argv[1], sys.argv[2], sys.argv[3]
 launches_per_step = float(sys.argv[4]) if len(sys.argv) > 4 else 1.0
 KERNELS = ("hash_var", "bloom_bin", "bloom_tile", "bloom_probe_multi", "pb_desc", "pb_hist", "pb_rows", "pb_scan",
+           "pb_colsum", "pb_plan", "pb_starts",
            "pb_scatter", "pb_bin", "pb_tile", "pb_gather")
 acc = defaultdict(lambda: defaultdict(list))
 for f in glob.glob(os.path.join(root, "p*", "**", "*counter_collection.csv"), recursive=True):

@@ -3,7 +3,7 @@
 # its answer stores / bitmap loads / entry loads (wrong answers; timing only).
 set -u
 cd "$(dirname "$0")/.."
-OUT=gpurun_out/r02/pbexp
+OUT=gpurun_out/${TAG:-r02/pbexp}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 for e in 0 1 2 4 7; do
