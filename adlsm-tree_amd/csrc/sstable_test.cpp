@@ -8,6 +8,12 @@
 //   sstable_test bench <n> <dir>     flush an n-entry memtable ("key%012d" / 100-byte
 //                                    values, seq = i): prints one JSON line with the
 //                                    time of the Add loop and of Final (GPU filter)
+//   sstable_test overlap <dir>       both memtables as two outputs of one compaction:
+//                                    table 2 is filled while table 1's filter builds
+//                                    (BeginFinal / EndFinal); prints "<oid> <bytes>" twice
+//   sstable_test pipebench <n> <t>   t tables of n entries written one after another,
+//                                    Final per table vs BeginFinal, fill the next
+//                                    table, EndFinal: one JSON line with both times
 //
 // tests/test_gpu_parity.py compares the file byte for byte with the oracle
 // (oracle/sstable_oracle.py) and the oid with SURVEY.md Appendix B.
@@ -18,6 +24,7 @@
 #include <algorithm>
 #include <chrono>
 #include <fstream>
+#include <memory>
 #include <sstream>
 #include <string>
 #include <vector>
@@ -118,6 +125,77 @@ int main(int argc, char **argv) {
     }
     printf("{\"entries\": %ld, \"bytes\": %d, \"oid\": \"%s\", \"add_s\": %.6f, \"final_s\": %.6f, \"filter_s\": %.6f}\n",
            n, size, oid.c_str(), best_add, best_final, best_filter);
+    return 0;
+  }
+  if (argc == 3 && !strcmp(argv[1], "overlap")) {
+    const auto m1 = Memtable(1), m2 = Memtable(2);
+    PosixFileSink s1(argv[2]), s2(argv[2]);
+    if (s1.Open() || s2.Open()) return 1;
+    SSTableWriter w1(&s1, 10), w2(&s2, 10);
+    for (const auto &e : m1)
+      if (w1.Add(InnerKey(e), e.value)) return 1;
+    if (w1.BeginFinal()) return 1;
+    if (w1.Add(InnerKey(m1[0]), "x") != BAD_RECORD) return 3;  // no Add while the filter builds
+    for (const auto &e : m2)
+      if (w2.Add(InnerKey(e), e.value)) return 1;
+    unsigned char d1[32], d2[32];
+    if (w1.EndFinal(d1) || w2.BeginFinal() || w2.EndFinal(d2)) return 1;
+    if (w2.EndFinal(d2) != BAD_RECORD) return 3;  // one EndFinal per BeginFinal
+    printf("%s %d\n%s %d\n", Sha256Hex(d1).c_str(), w1.GetFileSize(), Sha256Hex(d2).c_str(), w2.GetFileSize());
+    return 0;
+  }
+  if (argc == 4 && !strcmp(argv[1], "pipebench")) {
+    const long n = atol(argv[2]);
+    const int tables = atoi(argv[3]);
+    std::vector<std::vector<std::string>> ikeys(tables), vals(tables);
+    char buf[32];
+    for (int t = 0; t < tables; ++t)
+      for (long i = 0; i < n; ++i) {
+        snprintf(buf, sizeof buf, "k%03d%012ld", t, i);
+        ikeys[t].push_back(InnerKey({buf, (int64_t)i, 0, ""}));
+        vals[t].push_back(std::string(100, (char)('a' + (i + t) % 26)));
+      }
+    auto fill = [&](SSTableWriter &w, int t) {
+      for (long i = 0; i < n; ++i)
+        if (w.Add(ikeys[t][i], vals[t][i])) return false;
+      return true;
+    };
+    double best_seq = 1e30, best_pipe = 1e30;
+    std::vector<std::string> oid_seq(tables), oid_pipe(tables);
+    for (int rep = 0; rep < 4; ++rep) {  // rep 0 warms the device up
+      {  // Final per table
+        std::vector<StringSink> sinks(tables);
+        const auto t0 = std::chrono::steady_clock::now();
+        for (int t = 0; t < tables; ++t) {
+          SSTableWriter w(&sinks[t], 10);
+          unsigned char d[32];
+          if (!fill(w, t) || w.Final(d)) return 1;
+          oid_seq[t] = Sha256Hex(d);
+        }
+        if (rep) best_seq = std::min(best_seq, std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
+      }
+      {  // table t+1 filled while table t's filter builds
+        std::vector<StringSink> sinks(tables);
+        std::vector<std::unique_ptr<SSTableWriter>> ws;
+        for (int t = 0; t < tables; ++t) ws.push_back(std::make_unique<SSTableWriter>(&sinks[t], 10));
+        const auto t0 = std::chrono::steady_clock::now();
+        for (int t = 0; t < tables; ++t) {
+          if (!fill(*ws[t], t) || ws[t]->BeginFinal()) return 1;
+          if (t) {
+            unsigned char d[32];
+            if (ws[t - 1]->EndFinal(d)) return 1;
+            oid_pipe[t - 1] = Sha256Hex(d);
+          }
+        }
+        unsigned char d[32];
+        if (ws[tables - 1]->EndFinal(d)) return 1;
+        oid_pipe[tables - 1] = Sha256Hex(d);
+        if (rep) best_pipe = std::min(best_pipe, std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
+      }
+      if (oid_seq != oid_pipe) return 4;
+    }
+    printf("{\"entries_per_table\": %ld, \"tables\": %d, \"final_per_table_s\": %.6f, \"overlapped_s\": %.6f, "
+           "\"oids_equal\": true}\n", n, tables, best_seq, best_pipe);
     return 0;
   }
   int a = 1;

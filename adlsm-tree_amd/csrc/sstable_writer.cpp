@@ -155,7 +155,7 @@ SSTableWriter::SSTableWriter(Sink *sink, unique_ptr<FilterAlgorithm> &&filter)
 /* src/sstable.cpp:26-35: the user key (inner key minus seq and op,
  * src/keys.cpp:7-9) goes to the filter, the entry to the data block. */
 RC SSTableWriter::Add(string_view inner_key, string_view value) {
-  if (inner_key.size() < 9) return BAD_RECORD;
+  if (inner_key.size() < 9 || filter_job_.valid()) return BAD_RECORD;
   filter_block_.Update(inner_key.substr(0, inner_key.size() - 9));
   RC rc = data_block_.Add(inner_key, value);
   if (rc) return rc;
@@ -195,13 +195,29 @@ RC SSTableWriter::FlushDataBlock() {
 /* src/sstable.cpp:54-99: data tail, filter block (GPU build), meta block
  * ("filter" -> handle), index block, footer; the oid is the SHA-256 of it all. */
 RC SSTableWriter::Final(unsigned char sha256_digit[32]) {
+  if (RC rc = BeginFinal()) return rc;
+  return EndFinal(sha256_digit);
+}
+
+RC SSTableWriter::BeginFinal() {
+  if (filter_job_.valid()) return BAD_RECORD;
   RC rc;
   if (!data_block_.Empty() && (rc = FlushDataBlock())) return rc;
+  // the worker owns filter_block_ and filter_out_ until EndFinal's get()
+  filter_job_ = std::async(std::launch::async, [this] {
+    const auto f0 = std::chrono::steady_clock::now();
+    const RC r = filter_block_.Final(filter_out_);  // the reference drops this RC
+    filter_seconds_ = std::chrono::duration<double>(std::chrono::steady_clock::now() - f0).count();
+    return r;
+  });
+  return OK;
+}
 
-  const auto f0 = std::chrono::steady_clock::now();
-  rc = filter_block_.Final(buffer_);  // the reference drops this RC
-  filter_seconds_ = std::chrono::duration<double>(std::chrono::steady_clock::now() - f0).count();
+RC SSTableWriter::EndFinal(unsigned char sha256_digit[32]) {
+  if (!filter_job_.valid()) return BAD_RECORD;
+  RC rc = filter_job_.get();
   if (rc) return rc;
+  buffer_ = std::move(filter_out_);
   if ((rc = Emit(buffer_))) return rc;
   filter_block_handle_.SetMeta(offset_, (int)buffer_.size());
   offset_ += (int)buffer_.size();

@@ -19,6 +19,7 @@
 #pragma once
 #include <stdint.h>
 
+#include <future>
 #include <memory>
 #include <string>
 #include <string_view>
@@ -140,6 +141,15 @@ class SSTableWriter {
   RC AddBatch(const char *keys, const uint64_t *key_off, const char *values, const uint64_t *val_off,
               size_t n);
   RC Final(unsigned char sha256_digit[32]);
+  /* Final() in two halves (Final == BeginFinal + EndFinal), so a caller that
+   * writes several tables -- a compaction's outputs, src/db.cpp:428-509 --
+   * can fill the next table while this one's filter builds on the GPU.
+   * BeginFinal flushes the data tail and starts the filter build on a worker
+   * thread; EndFinal waits for it and writes the filter, meta, index and
+   * footer blocks.  No Add between the two (BAD_RECORD); the file and its oid
+   * are the same as Final's. */
+  RC BeginFinal();
+  RC EndFinal(unsigned char sha256_digit[32]);
   int GetFileSize() const { return offset_; }
   /* wall time of the filter block build inside the last Final() */
   double filter_seconds() const { return filter_seconds_; }
@@ -158,6 +168,10 @@ class SSTableWriter {
   string last_key_;
   string buffer_;
   double filter_seconds_ = 0;
+  /* BeginFinal's build and its block (declared in this order so the future,
+   * whose destructor waits for the build, goes first) */
+  string filter_out_;
+  future<RC> filter_job_;
   static constexpr size_t need_flush_size_ = 1u << 12; /* 4KB, src/sstable.hpp:40 */
 };
 

@@ -754,6 +754,25 @@ def test_sstable_writer_file_parity(dev, golden, oracle, tmp_path, mode, which):
         assert oid == golden["appendix_b"]["sstable_test"]["oid"]
 
 
+def test_sstable_writer_overlapped_final(dev, golden, oracle, tmp_path):
+    """Two outputs of one compaction: table 2 is filled while table 1's filter
+    builds on the GPU (SSTableWriter::BeginFinal / EndFinal).  Both files are
+    byte-identical to the oracle's and carry the oids a plain Final gives."""
+    import sstable_oracle as S
+
+    exe = os.path.join(ROOT, "adlsm-tree_amd", "bin", "sstable_test")
+    r = subprocess.run([exe, "overlap", str(tmp_path)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    lines = r.stdout.split("\n")
+    for which, line in zip((1, 2), lines):
+        oid, size = line.split()
+        got = (tmp_path / (oid + ".sst")).read_bytes()
+        want = S.sstable_bytes(S.sstable_test_entries(which))
+        assert len(got) == int(size) and got == want, which
+        assert hashlib.sha256(got).hexdigest() == oid
+    assert lines[0].split()[0] == golden["appendix_b"]["sstable_test"]["oid"]
+
+
 def test_concurrent_probes_and_builds(dev):
     """SURVEY.md §8b threading: 8 threads probing one FilterBlockReader while 2
     threads build filter blocks; every result equals the sequential one."""
