@@ -375,7 +375,11 @@ __global__ __launch_bounds__(kBlk) void pb_scatter_kernel(const uint4 *__restric
                                                           uint32_t nb, const PFilter *__restrict__ desc,
                                                           const uint32_t *__restrict__ cnt,
                                                           const uint32_t *__restrict__ start,
-                                                          uint16_t *__restrict__ dest, uint2 *__restrict__ hs) {
+                                                          uint16_t *__restrict__ dest, uint2 *__restrict__ hs,
+                                                          uint32_t exp) {
+#ifndef ADL_BLOOM_STAMPS
+  exp = 0;  // diagnostics build only (wrong answers): 8 no hashing, 16 no run stores, 32 no place stores
+#endif
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   uint2 *lhs = reinterpret_cast<uint2 *>(lds);  // kQB hashes in the block's filter order
   uint32_t *lcnt = lds + 2 * kQB, *lstart = lcnt + F + 1, *lbase = lstart + F + 1, *lcur = lbase + F + 1;
@@ -405,14 +409,20 @@ __global__ __launch_bounds__(kBlk) void pb_scatter_kernel(const uint4 *__restric
       if (b < F) {
         place = (uint16_t)atomicAdd(&lcur[b], 1u);
         uint32_t h1, h2;
-        hash16(kq[r], h1, h2);
+        if (exp & 8) {
+          h1 = kq[r].x;
+          h2 = kq[r].y;
+        } else {
+          hash16(kq[r], h1, h2);
+        }
         lhs[place] = make_uint2(h1, h2);
       }
-      dest[i] = place;
+      if (!(exp & 32)) dest[i] = place;
     }
   }
   __syncthreads();
   // run by run: consecutive lanes write consecutive slots (whole lines)
+  if (exp & 16) return;
   for (uint32_t f = wave; f < F; f += kBlk / kWave) {
     const uint32_t c = lcnt[f], lb = lbase[f], gs = lstart[f];
     for (uint32_t r = lane; r < c; r += kWave) hs[gs + r] = lhs[lb + r];
@@ -836,17 +846,18 @@ int adl_bloom_probe_batch_device(const uint8_t *d_keys, const uint64_t *d_offset
       ADL_HIP_TRY(hipGetLastError());
     }
     if (int rc = adl_host::lds_limit<pb_scatter_kernel>()) return rc;
+    const char *exp_env = getenv("ADL_PB_EXP");  // diagnostics build only
+    const uint32_t exp = exp_env ? (uint32_t)atoi(exp_env) : 0u;
     hipLaunchKernelGGL(pb_scatter_kernel, dim3(p.nb), dim3(kBlk), lds_k3, st, reinterpret_cast<const uint4 *>(d_keys),
-                       d_filter_id, n, F, p.nb, desc, cnt, start, dest, hs);
+                       d_filter_id, n, F, p.nb, desc, cnt, start, dest, hs, exp);
     ADL_HIP_TRY(hipGetLastError());
     auto p1 = p.k == 6 ? pb_bin_kernel<6> : pb_bin_kernel<0>;
     if (int rc = p.k == 6 ? adl_host::lds_limit<pb_bin_kernel<6>>() : adl_host::lds_limit<pb_bin_kernel<0>>()) return rc;
     hipLaunchKernelGGL(p1, dim3(cus), dim3(kBlk), lds_p1, st, hs, desc, cf, scal, p.k, p.C, ent, tab, res);
     ADL_HIP_TRY(hipGetLastError());
     if (int rc = adl_host::lds_limit<pb_tile_kernel>()) return rc;
-    const char *exp_env = getenv("ADL_PB_EXP");  // diagnostics build only
     hipLaunchKernelGGL(pb_tile_kernel, dim3(cus), dim3(kBlk), lds_p2, st, d_bitmaps, desc, F, scal, p.k, p.C, ent,
-                       tab, res, exp_env ? (uint32_t)atoi(exp_env) : 0u);
+                       tab, res, exp);
     ADL_HIP_TRY(hipGetLastError());
     if (int rc = adl_host::lds_limit<pb_gather_kernel>()) return rc;
     hipLaunchKernelGGL(pb_gather_kernel, dim3(p.nb), dim3(kBlk), lds_k6, st, dest, res, n, F, p.nb, cnt, start,

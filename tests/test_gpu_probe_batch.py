@@ -116,3 +116,17 @@ def test_probe_batch_ranges_with_gaps(dev, ab, oracle):
     got = ab.probe_batch(d(keys), d(fid.view(np.int32)), d(arena), d(np.array(begin, np.int64)),
                          bitmap_end=d(np.array(end, np.int64))).cpu().numpy()
     assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("F", [1500, 4096])
+def test_probe_batch_many_filters(dev, ab, oracle, F):
+    """Many filters: more per-filter counters than threads in K1 / K3 / K6
+    (F + 1 > 1024), up to the binned probe's limit of 4096."""
+    sizes = [(t * 37) % 300 for t in range(F)]  # 0..299 keys, some empty
+    arena, off = _arena(oracle, sizes, seed0=4242)
+    rng = np.random.default_rng(F)
+    n = (1 << 20) + 777
+    fid = rng.integers(0, F, n).astype(np.uint32)
+    keys = oracle.splitmix_keys16(6, n)
+    _check(dev, ab, oracle, arena, off, keys, fid)
+
