@@ -616,10 +616,27 @@ __global__ __launch_bounds__(kBlk) void pb_tile_kernel(const uint8_t *__restrict
       pre[u] = (v < r.nvec && !(exp & 2)) ? load_nt(src + v) : make_uint4(0, 0, 0, 0);
     }
   };
+  // The first 64 runs of this wave in a tile: lane q holds run q's (start,
+  // end) from the (tile, chunk) table.  They are loaded with the tile's
+  // bitmap, one tile ahead, so a tile starts with no table round trip.
+  const uint32_t wv = __builtin_amdgcn_readfirstlane((uint32_t)wave);  // (SGPR: the stage cursor below is scalar)
+  uint32_t pre_rs = 0, pre_re = 0;
+  auto prefetch_rows = [&](const TileRef &r) {
+    const PFilter &dn = desc[r.f];
+    const uint32_t nc = dn.nchunks;
+    const uint32_t nq = nc > wv ? (nc - wv + NW - 1) / NW : 0u;
+    if (nq) {
+      const uint32_t *row = table + dn.table_base + (uint64_t)r.t * nc;
+      const uint32_t jc = wv + NW * min((uint32_t)lane, min((uint32_t)kWave, nq) - 1u);
+      pre_rs = row[jc];
+      pre_re = row[nc + jc];
+    }
+  };
   TileRef cur{};
   if (slot < total_tiles) {
     cur = tile_ref(desc, ltb, F, slot);
     prefetch(cur);
+    prefetch_rows(cur);
   }
   for (uint32_t g = slot; g < total_tiles; g += G) {
     __syncthreads();  // the previous tile's lookups are done
@@ -632,15 +649,17 @@ __global__ __launch_bounds__(kBlk) void pb_tile_kernel(const uint8_t *__restrict
     if ((uint32_t)tid < cur.tail)
       reinterpret_cast<uint8_t *>(ltile)[cur.nvec * 16 + tid] = bitmaps[cur.a0 + cur.nvec * 16 + tid];
     const TileRef now = cur;
+    const uint32_t now_rs = pre_rs, now_re = pre_re;
     if (g + G < total_tiles) {
       cur = tile_ref(desc, ltb, F, g + G);
       prefetch(cur);
+      prefetch_rows(cur);
     }
     const PFilter d = desc[now.f];
     const uint32_t nc = d.nchunks;
     const uint32_t *row = table + d.table_base + (uint64_t)now.t * nc;
     // this wave's runs: chunks wave + NW*q; lane q holds run q's (start, end)
-    const uint32_t nq = nc > (uint32_t)wave ? (nc - wave + NW - 1) / NW : 0u;
+    const uint32_t nq = nc > wv ? (nc - wv + NW - 1) / NW : 0u;
     __syncthreads();  // the tile is in LDS
     // Two-stage pipeline over the wave's runs cut into stages of at most
     // kRunLoads x 64 entries (a long run is several stages): stage s+1's loads
@@ -674,15 +693,16 @@ __global__ __launch_bounds__(kBlk) void pb_tile_kernel(const uint8_t *__restrict
 #pragma unroll
       for (int u = 0; u < kRunLoads; ++u) {
         const uint32_t bit = (sg.x[u] & ((1u << kTL) - 1u)) + now.sh;
-        const bool clr = sg.b0 + u * kWave + lane < sg.b1 && !((w[u] >> (bit & 31)) & 1u) && !(exp & 1);
+        // bitwise, not short-circuit: no branch per entry
+        const bool clr = (sg.b0 + u * kWave + lane < sg.b1) & (((w[u] >> (bit & 31)) & 1u) == 0u) & !(exp & 1);
         zero_answer(clr, rq + (sg.x[u] >> kTL));
       }
     };
     for (uint32_t q0 = 0; q0 < nq; q0 += kWave) {
       const uint32_t nr = min((uint32_t)kWave, nq - q0);
-      uint32_t rs, re;
-      {
-        const uint32_t jc = wave + NW * (q0 + min((uint32_t)lane, nr - 1u));
+      uint32_t rs = now_rs, re = now_re;  // the first 64 runs came with the tile
+      if (q0) {
+        const uint32_t jc = wv + NW * (q0 + min((uint32_t)lane, nr - 1u));
         rs = row[jc];
         re = row[nc + jc];
       }
@@ -693,7 +713,7 @@ __global__ __launch_bounds__(kBlk) void pb_tile_kernel(const uint8_t *__restrict
         const uint32_t qe = more ? __builtin_amdgcn_readlane(re, sq) : 0u;
         const uint32_t b0 = more ? so : 0u;
         const uint32_t b1 = more ? min(so + (uint32_t)(kRunLoads * kWave), qe) : 0u;
-        const uint32_t jc = wave + NW * (q0 + (more ? sq : nr - 1u));
+        const uint32_t jc = wv + NW * (q0 + (more ? sq : nr - 1u));
         issue(sg, b0, b1, jc);
         if (more) {
           so = b1;
