@@ -20,6 +20,10 @@ timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('s
 tail -n 1 "$OUT/smoke.log"
 step readpath
 timeout -k 10 300 adlsm-tree_amd/bin/readpath_test --bench > "$OUT/readpath_bench.json" 2> "$OUT/readpath_bench.err" || exit 1
+step sstable_pipebench
+for nt in "100000 8" "1000000 4"; do
+  timeout -k 10 300 adlsm-tree_amd/bin/sstable_test pipebench $nt >> "$OUT/sstable_pipebench.jsonl" || exit 1
+done
 step bench_all
 bash tools/bench_all.sh || exit 1
 cp gpurun_out/bench_all.jsonl "$OUT/bench_all.jsonl"
