@@ -669,8 +669,10 @@ __global__ __launch_bounds__(kBlk) void pb_tile_kernel(const uint8_t *__restrict
     struct Stage {
       uint32_t x[kRunLoads];
       uint32_t b0, b1, jc;
+      bool live;  // a stage of a run (possibly empty); false past the batch's last run
     };
-    auto issue = [&](Stage &sg, uint32_t b0, uint32_t b1, uint32_t jc) {
+    auto issue = [&](Stage &sg, uint32_t b0, uint32_t b1, uint32_t jc, bool live) {
+      sg.live = live;
       sg.b0 = b0;
       sg.b1 = b1;
       sg.jc = jc;
@@ -714,7 +716,7 @@ __global__ __launch_bounds__(kBlk) void pb_tile_kernel(const uint8_t *__restrict
         const uint32_t b0 = more ? so : 0u;
         const uint32_t b1 = more ? min(so + (uint32_t)(kRunLoads * kWave), qe) : 0u;
         const uint32_t jc = wv + NW * (q0 + (more ? sq : nr - 1u));
-        issue(sg, b0, b1, jc);
+        issue(sg, b0, b1, jc, more);
         if (more) {
           so = b1;
           if (so >= qe) {
@@ -723,9 +725,12 @@ __global__ __launch_bounds__(kBlk) void pb_tile_kernel(const uint8_t *__restrict
           }
         }
       };
+      // An empty run (a chunk with no entry in this tile) is a live stage with
+      // nothing to test: the loop ends only past the last run, not at the
+      // first empty stage.
       Stage A, B;
       take(A);
-      while (A.b1 > A.b0) {
+      while (A.live) {
         take(B);
         consume(A);
         take(A);

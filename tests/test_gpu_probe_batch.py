@@ -130,3 +130,19 @@ def test_probe_batch_many_filters(dev, ab, oracle, F):
     keys = oracle.splitmix_keys16(6, n)
     _check(dev, ab, oracle, arena, off, keys, fid)
 
+
+
+@pytest.mark.parametrize("bpk", [1, 3])
+def test_probe_batch_sparse_runs(dev, ab, oracle, bpk):
+    """One filter of 2^30 bits (1 024 tiles) and k = 1 or 2: a chunk of 4 096
+    queries puts 4-8 entries into each tile, so many (tile, chunk) runs are
+    empty, also several in a row for one wave of pb_tile.  The bitmap is random
+    bytes (half its bits set) rather than a built filter, so every skipped run
+    would show as answers of 1 where the reference answers 0."""
+    rng = np.random.default_rng(31 + bpk)
+    arena = rng.integers(0, 256, (1 << 27) + 16, dtype=np.uint8)
+    off = np.array([0, 1 << 27], np.uint64)
+    n = (1 << 20) + 200_000
+    keys = oracle.splitmix_keys16(99, n)
+    fid = np.zeros(n, np.uint32)
+    _check(dev, ab, oracle, arena, off, keys, fid, bpk=bpk)
