@@ -61,6 +61,7 @@ constexpr uint32_t kSentinel = 0xFFFFFFFFu;
 constexpr uint16_t kNoSlot = 0xFFFF;            // a query that is answered 0 without probing
 constexpr uint32_t kLdsWords = 40960;           // 160 KiB
 constexpr uint64_t kMinBinned = 1ull << 20;     // below this the direct kernel wins
+constexpr uint32_t kSplit6 = 0;                 // k = 6: bits in the first of two rounds (0: one round)
 
 struct PFilter {
   uint32_t m, magic, shift, tiles;
@@ -432,12 +433,17 @@ __global__ __launch_bounds__(kBlk) void pb_scatter_kernel(const uint4 *__restric
 // ---------------------------------------------------------------- P1
 // Persistent: workgroup b takes chunks b, b + G, ...; the next chunk's hashes
 // are in flight into registers while the current one is sorted and stored.
+// Rounds (the batched form of the reference's stop at the first clear bit,
+// src/filter_block.cpp:54-59): round 0 bins all k bits of every query; round 1
+// bins bits j0 .. j0+KFIX of every query and sets its answer to 1; round 2
+// bins bits j0 .. j0+KFIX of the queries whose answer round 1's pb_tile left
+// at 1.  KFIX = 0: all k bits, round 0 only.
 template <int KFIX>
 __global__ __launch_bounds__(kBlk) void pb_bin_kernel(const uint2 *__restrict__ hs, const PFilter *__restrict__ desc,
                                                       const uint32_t *__restrict__ chunk_filter,
                                                       const uint32_t *__restrict__ scal, uint32_t k, uint32_t C,
                                                       uint32_t *__restrict__ ent, uint32_t *__restrict__ table,
-                                                      uint8_t *__restrict__ res) {
+                                                      uint8_t *__restrict__ res, uint32_t j0, uint32_t round) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   uint32_t *hist = lds;                          // kMaxTiles + 1 counters, later cursors
   uint32_t *scratch = lds + kMaxTiles + 4;       // scan scratch (64 words)
@@ -447,7 +453,9 @@ __global__ __launch_bounds__(kBlk) void pb_bin_kernel(const uint2 *__restrict__ 
   const int tid = threadIdx.x;
   const uint32_t total_chunks = scal[1];
   const uint32_t G = gridDim.x;
-  auto fetch = [&](uint32_t c, uint2 (&h)[kCPT]) {
+  // the answers round 1 left (round 2), loaded with the hashes
+  const bool filt = round == 2;
+  auto fetch = [&](uint32_t c, uint2 (&h)[kCPT], uint8_t (&al)[kCPT]) {
     if (c >= total_chunks) return;
     const uint32_t f = chunk_filter[c];
     const uint32_t j = c - desc[f].chunk_base;
@@ -455,17 +463,20 @@ __global__ __launch_bounds__(kBlk) void pb_bin_kernel(const uint2 *__restrict__ 
     const uint32_t cnt = min(C, desc[f].cnt - j * C);
 #pragma unroll
     for (uint32_t r = 0; r < kCPT; ++r) {
-      const uint32_t q = tid + r * kBlk;
-      h[r] = hs[q0 + min(q, cnt - 1u)];
+      const uint32_t q = q0 + min(tid + r * kBlk, cnt - 1u);
+      h[r] = hs[q];
+      al[r] = filt ? res[q] : (uint8_t)1;
     }
   };
   uint2 nxt[kCPT];
-  fetch(blockIdx.x, nxt);
+  uint8_t nal[kCPT];
+  fetch(blockIdx.x, nxt, nal);
   for (uint32_t c = blockIdx.x; c < total_chunks; c += G) {
     uint2 cur[kCPT];
+    bool live[kCPT];
 #pragma unroll
-    for (uint32_t r = 0; r < kCPT; ++r) cur[r] = nxt[r];
-    fetch(c + G, nxt);
+    for (uint32_t r = 0; r < kCPT; ++r) cur[r] = nxt[r], live[r] = nal[r] != 0;
+    fetch(c + G, nxt, nal);
     const uint32_t f = chunk_filter[c];
     const PFilter d = desc[f];
     const uint32_t j = c - d.chunk_base;
@@ -476,17 +487,19 @@ __global__ __launch_bounds__(kBlk) void pb_bin_kernel(const uint2 *__restrict__ 
     __syncthreads();  // the previous chunk's entries are read out of lpos
     for (uint32_t t = tid; t <= T; t += kBlk) hist[t] = 0;
 #pragma unroll
-    for (uint32_t r = 0; r < kCPT; ++r)
-      if (tid + r * kBlk < cnt) res[q0 + tid + r * kBlk] = 1;
+    for (uint32_t r = 0; r < kCPT; ++r) {
+      if (!filt && tid + r * kBlk < cnt) res[q0 + tid + r * kBlk] = 1;
+      live[r] = live[r] && tid + r * kBlk < cnt;
+    }
     __syncthreads();
     uint32_t pos[kCPT][KR];
 #pragma unroll
     for (uint32_t r = 0; r < kCPT; ++r) {
-      if (tid + r * kBlk < cnt) {
+      if (live[r]) {
         if constexpr (KFIX > 0) {
 #pragma unroll
           for (int jj = 0; jj < KFIX; ++jj) {
-            pos[r][jj] = fastmod(cur[r].x + (uint32_t)jj * cur[r].y, mod);
+            pos[r][jj] = fastmod(cur[r].x + (j0 + (uint32_t)jj) * cur[r].y, mod);
             atomicAdd(&hist[pos[r][jj] >> kTL], 1u);
           }
         } else {
@@ -502,7 +515,7 @@ __global__ __launch_bounds__(kBlk) void pb_bin_kernel(const uint2 *__restrict__ 
 #pragma unroll
     for (uint32_t r = 0; r < kCPT; ++r) {
       const uint32_t q = tid + r * kBlk;
-      if (q < cnt) {
+      if (live[r]) {
         if constexpr (KFIX > 0) {
           uint32_t sl[KFIX];
 #pragma unroll
@@ -876,14 +889,36 @@ int adl_bloom_probe_batch_device(const uint8_t *d_keys, const uint64_t *d_offset
     hipLaunchKernelGGL(pb_scatter_kernel, dim3(p.nb), dim3(kBlk), lds_k3, st, reinterpret_cast<const uint4 *>(d_keys),
                        d_filter_id, n, F, p.nb, desc, cnt, start, dest, hs, exp);
     ADL_HIP_TRY(hipGetLastError());
-    auto p1 = p.k == 6 ? pb_bin_kernel<6> : pb_bin_kernel<0>;
-    if (int rc = p.k == 6 ? adl_host::lds_limit<pb_bin_kernel<6>>() : adl_host::lds_limit<pb_bin_kernel<0>>()) return rc;
-    hipLaunchKernelGGL(p1, dim3(cus), dim3(kBlk), lds_p1, st, hs, desc, cf, scal, p.k, p.C, ent, tab, res);
-    ADL_HIP_TRY(hipGetLastError());
+    // k = 6: two rounds, bits 0 .. split-1 of every query, then the rest for
+    // the queries still answered 1 (ADL_PB_SPLIT = 0: one round of all k)
+    const char *split_env = getenv("ADL_PB_SPLIT");
+    const uint32_t split = p.k == 6 ? (split_env ? (uint32_t)atoi(split_env) : kSplit6) : 0u;
+    if (split > 2) return ADL_ERR_INVALID_ARG;
     if (int rc = adl_host::lds_limit<pb_tile_kernel>()) return rc;
-    hipLaunchKernelGGL(pb_tile_kernel, dim3(cus), dim3(kBlk), lds_p2, st, d_bitmaps, desc, F, scal, p.k, p.C, ent,
-                       tab, res, exp);
-    ADL_HIP_TRY(hipGetLastError());
+    using BinK = decltype(&pb_bin_kernel<6>);
+    auto bin = [&](BinK kern, int lds_rc, uint32_t j0, uint32_t round) -> int {
+      if (lds_rc) return lds_rc;
+      hipLaunchKernelGGL(kern, dim3(cus), dim3(kBlk), lds_p1, st, hs, desc, cf, scal, p.k, p.C, ent, tab, res, j0,
+                         round);
+      ADL_HIP_TRY(hipGetLastError());
+      hipLaunchKernelGGL(pb_tile_kernel, dim3(cus), dim3(kBlk), lds_p2, st, d_bitmaps, desc, F, scal, p.k, p.C, ent,
+                         tab, res, exp);
+      ADL_HIP_TRY(hipGetLastError());
+      return ADL_OK;
+    };
+    int rc_bin;
+    if (split == 1) {
+      if ((rc_bin = bin(pb_bin_kernel<1>, adl_host::lds_limit<pb_bin_kernel<1>>(), 0u, 1u)) != ADL_OK) return rc_bin;
+      rc_bin = bin(pb_bin_kernel<5>, adl_host::lds_limit<pb_bin_kernel<5>>(), 1u, 2u);
+    } else if (split == 2) {
+      if ((rc_bin = bin(pb_bin_kernel<2>, adl_host::lds_limit<pb_bin_kernel<2>>(), 0u, 1u)) != ADL_OK) return rc_bin;
+      rc_bin = bin(pb_bin_kernel<4>, adl_host::lds_limit<pb_bin_kernel<4>>(), 2u, 2u);
+    } else if (p.k == 6) {
+      rc_bin = bin(pb_bin_kernel<6>, adl_host::lds_limit<pb_bin_kernel<6>>(), 0u, 0u);
+    } else {
+      rc_bin = bin(pb_bin_kernel<0>, adl_host::lds_limit<pb_bin_kernel<0>>(), 0u, 0u);
+    }
+    if (rc_bin != ADL_OK) return rc_bin;
     if (int rc = adl_host::lds_limit<pb_gather_kernel>()) return rc;
     hipLaunchKernelGGL(pb_gather_kernel, dim3(p.nb), dim3(kBlk), lds_k6, st, dest, res, n, F, p.nb, cnt, start,
                        d_out);
