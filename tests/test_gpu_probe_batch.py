@@ -168,3 +168,21 @@ def test_probe_batch_two_rounds(dev, ab, oracle, split, monkeypatch):
         if sz and sel.size:
             keys[sel] = oracle.splitmix_keys16(1234 + t, sz)[rng.integers(0, sz, sel.size)]
     _check(dev, ab, oracle, arena, off, keys, fid)
+
+
+def test_probe_batch_many_chunks_one_filter(dev, ab, oracle):
+    """One filter with more than 64 chunks per pb_tile wave (5.4 M queries:
+    about 1 300 chunks of 4 096, 16 waves), so every wave stages its runs in
+    several batches of 64 (the row loads past the prefetched first batch)."""
+    sizes = [300_000, 5]
+    arena, off = _arena(oracle, sizes, seed0=2718)
+    rng = np.random.default_rng(27)
+    n = 6_000_000
+    fid = (rng.random(n) < 0.1).astype(np.uint32)  # 90 % to filter 0
+    keys = oracle.splitmix_keys16(28, n)
+    ins = rng.random(n) < 0.5
+    for t, sz in enumerate(sizes):
+        sel = np.nonzero(ins & (fid == t))[0]
+        keys[sel] = oracle.splitmix_keys16(2718 + t, sz)[rng.integers(0, sz, sel.size)]
+    got = _check(dev, ab, oracle, arena, off, keys, fid)
+    assert got[ins].all()
