@@ -45,7 +45,7 @@ EXPORTS = (
     "adl_synth_varlen_lengths_device", "adl_synth_varlen_fill_device",
     "adl_bloom_profile_enable", "adl_bloom_profile_collect", "adl_synth_probe_queries_device",
     "adl_bloom_profile_each", "adl_bloom_probe_batch_workspace_bytes", "adl_bloom_probe_batch_device",
-    "adl_bloom_test_fault", "adl_bloom_build_positions",
+    "adl_bloom_test_fault", "adl_bloom_build_positions", "adl_bloom_get_device", "adl_bloom_set_device",
 )
 
 _LIB = None
@@ -112,6 +112,8 @@ def lib() -> ctypes.CDLL:
         "adl_bloom_profile_each": (ctypes.c_int, [ctypes.POINTER(ctypes.c_double), u32, ctypes.POINTER(u32)]),
         "adl_bloom_test_fault": (ctypes.c_int, [ctypes.c_int, ctypes.c_int64]),
         "adl_bloom_build_positions": (ctypes.c_int, [vp, u32, i32, vp, ctypes.POINTER(u64), vp]),
+        "adl_bloom_get_device": (ctypes.c_int, [ctypes.POINTER(i32)]),
+        "adl_bloom_set_device": (ctypes.c_int, [i32]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

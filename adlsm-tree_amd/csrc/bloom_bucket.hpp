@@ -1,0 +1,32 @@
+// adlsm-tree_amd/csrc/bloom_bucket.hpp -- library-internal interface of the
+// bucketed build (bloom_bucket.hip), the default build for 16-byte keys.
+//
+// Same output as BloomFilter::Keys2Block (reference src/filter_block.cpp:9-33)
+// per filter; bloom_build.hip's build_groups dispatches a group of filters
+// here when bk_plan accepts it and falls back to its chunk/table build
+// otherwise (large filters, other key shapes, adjacent-duplicate skipping).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace adl_bk {
+
+// Workspace bytes the bucketed build needs for these filters, or 0 when it
+// does not take them (a filter of more than kMaxTiles tiles, or the LDS
+// budget).  Key shape is not an input: the caller checks that separately.
+__attribute__((visibility("hidden"))) uint64_t workspace_bytes(const uint64_t *counts, uint32_t nf, int32_t bpk);
+
+// Build the filters of one group from 16-byte-aligned 16-byte keys.
+// key_begin[nf+1], bitmap_off[nf] (16-byte multiples).  ev: 4 events (pass A
+// start/stop, pass B start/stop) or nullptr.  Returns ADL_* status;
+// ADL_ERR_TOO_LARGE when the group is not eligible.
+__attribute__((visibility("hidden"))) int build16(const uint4 *d_keys, const uint64_t *key_begin, uint32_t nf,
+                                                  int32_t bpk, uint8_t *d_bitmaps, const uint64_t *bitmap_off,
+                                                  void *ws, uint64_t ws_bytes, hipStream_t st, hipEvent_t *ev);
+
+// Sum of the entries the last build16 over these filters routed (the count
+// tables in the workspace); instrumentation for the bench line.
+__attribute__((visibility("hidden"))) int positions(const uint64_t *counts, uint32_t nf, int32_t bpk, const void *ws,
+                                                    uint64_t *out, hipStream_t st);
+
+}  // namespace adl_bk

@@ -40,6 +40,7 @@
 #include <type_traits>
 #include <vector>
 
+#include "bloom_bucket.hpp"
 #include "bloom_common.hpp"
 
 using namespace adl_dev;
@@ -1490,6 +1491,10 @@ namespace {
 // launch's workspace would overflow (groups of at most 2^31 / k keys).
 uint64_t group_keys_max(int32_t bpk) { return (1ull << 31) / (uint64_t)adl_host::num_probes(bpk); }
 
+// whether this thread's last group went through the bucketed build (for
+// adl_bloom_build_positions, which reads that build's tables)
+thread_local bool t_last_bk = false;
+
 int build_groups(const uint8_t *d_keys, const uint64_t *d_offsets, uint32_t key_stride,
                  const uint64_t *key_begin, uint32_t num_filters, int32_t bpk, uint8_t *d_bitmaps,
                  const uint64_t *bitmap_off, void *d_workspace, uint64_t workspace_bytes,
@@ -1513,6 +1518,25 @@ int build_groups(const uint8_t *d_keys, const uint64_t *d_offsets, uint32_t key_
       keys_in += c;
     }
     const uint32_t nf = e - g;
+    // 16-byte keys: the bucketed build (bloom_bucket.hip) when it takes the group
+    if (!atomic && !d_offsets && key_stride == 16 && (reinterpret_cast<uintptr_t>(d_keys) % 16) == 0 &&
+        !(flags & ADL_BLOOM_SKIP_ADJACENT_DUPLICATES) && adl_host::env_on("ADL_BLOOM_BK", true) &&
+        adl_bk::workspace_bytes(counts.data(), nf, bpk)) {
+      uint8_t *wsa = nullptr;
+      uint64_t wsb = 0;
+      if (d_workspace) {
+        wsa = reinterpret_cast<uint8_t *>(adl_host::round_up(reinterpret_cast<uintptr_t>(d_workspace), 256));
+        const uint64_t skip = (uint64_t)(wsa - static_cast<uint8_t *>(d_workspace));
+        wsb = workspace_bytes > skip ? workspace_bytes - skip : 0;
+      }
+      const int rc = adl_bk::build16(reinterpret_cast<const uint4 *>(d_keys), key_begin + g, nf, bpk, d_bitmaps,
+                                     bitmap_off + g, wsa, wsb, st, prof_slot());
+      if (rc) return rc;
+      t_last_bk = true;
+      g = e;
+      continue;
+    }
+    t_last_bk = false;
     Plan p;
     int rc = make_plan(counts.data(), nf, bpk, p);
     if (rc) return rc;
@@ -1582,6 +1606,20 @@ int adl_bloom_debug_stamps(uint64_t *out, uint64_t n) {
 
 int32_t adl_bloom_num_probes(int32_t bits_per_key) { return adl_host::num_probes(bits_per_key); }
 
+int adl_bloom_get_device(int32_t *device) {
+  if (!device) return ADL_ERR_INVALID_ARG;
+  int d = 0;
+  ADL_HIP_TRY(hipGetDevice(&d));
+  *device = d;
+  return ADL_OK;
+}
+
+int adl_bloom_set_device(int32_t device) {
+  if (device < 0) return ADL_ERR_INVALID_ARG;
+  ADL_HIP_TRY(hipSetDevice(device));
+  return ADL_OK;
+}
+
 uint64_t adl_bloom_bitmap_bytes(uint64_t n, int32_t bits_per_key) {
   return adl_host::bitmap_bytes(n, bits_per_key);
 }
@@ -1607,7 +1645,7 @@ uint64_t adl_bloom_build_workspace_bytes(const uint64_t *key_counts, uint32_t nu
     }
     Plan p;
     if (make_plan(key_counts + g, e - g, bits_per_key, p)) return 0;
-    ws = std::max(ws, p.ws_bytes);
+    ws = std::max({ws, p.ws_bytes, adl_bk::workspace_bytes(key_counts + g, e - g, bits_per_key)});
     g = e;
   }
   return ws;
@@ -1631,12 +1669,14 @@ int adl_bloom_build_positions(const uint64_t *key_counts, uint32_t num_filters, 
       g = g0;
       g0 = e;
     }
+    hipStream_t st = adl_host::sync_stream(stream);
+    const void *wsa = reinterpret_cast<const void *>(adl_host::round_up(reinterpret_cast<uintptr_t>(d_workspace), 256));
+    if (t_last_bk) return adl_bk::positions(key_counts + g, num_filters - g, bits_per_key, wsa, positions, st);
     Plan p;
     if (int rc = make_plan(key_counts + g, num_filters - g, bits_per_key, p)) return rc;
     const uint32_t *tab = reinterpret_cast<const uint32_t *>(
                               adl_host::round_up(reinterpret_cast<uintptr_t>(d_workspace), 256)) +
                           p.pos_words;
-    hipStream_t st = adl_host::sync_stream(stream);
     uint64_t sum = 0;
     std::vector<uint32_t> row;
     for (const FilterDesc &d : p.f) {  // row T of each filter's table: every chunk's total

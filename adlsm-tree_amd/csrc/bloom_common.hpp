@@ -6,18 +6,22 @@
 #include <atomic>
 #include <mutex>
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
 #include "../../include/adl_bloom.h"
 #include "murmur3_device.hpp"
 
-#define ADL_HIP_TRY(expr)                                \
-  do {                                                   \
-    hipError_t adl_e_ = (expr);                          \
-    if (adl_e_ != hipSuccess) {                          \
-      return adl_e_ == hipErrorOutOfMemory ? ADL_ERR_OUT_OF_MEMORY : ADL_ERR_DEVICE; \
-    }                                                    \
+// ADL_BLOOM_DEBUG=1: the HIP error behind a failed call goes to stderr
+#define ADL_HIP_TRY(expr)                                                                    \
+  do {                                                                                       \
+    hipError_t adl_e_ = (expr);                                                              \
+    if (adl_e_ != hipSuccess) {                                                              \
+      if (getenv("ADL_BLOOM_DEBUG"))                                                         \
+        fprintf(stderr, "adl_bloom: %s:%d: %s\n", __FILE__, __LINE__, hipGetErrorString(adl_e_)); \
+      return adl_e_ == hipErrorOutOfMemory ? ADL_ERR_OUT_OF_MEMORY : ADL_ERR_DEVICE;         \
+    }                                                                                        \
   } while (0)
 
 namespace adl_dev {

@@ -8,6 +8,7 @@
 #include <string.h>
 
 #include <atomic>
+#include <chrono>
 #include <map>
 #include <mutex>
 
@@ -184,6 +185,11 @@ RC FilterBlockWriter::Update(string_view key) {
   return OK;
 }
 
+RC FilterBlockWriter::UpdateBatch(const char *base, const uint64_t *off, size_t n, size_t trim) {
+  keys_.AddTrimmed(base, off, n, trim);
+  return OK;
+}
+
 /* src/filter_block.cpp:104-109 -- closes the current filter; its bitmap is
  * built with all the others in Final(). */
 RC FilterBlockWriter::Keys2Block() {
@@ -266,26 +272,34 @@ RC FilterCache::Probe(const vector<string_view> &oids, const vector<uint32_t> &t
 }
 
 FilterCache *FilterCache::Shared(int bits_per_key) {
+  struct Slot {
+    FilterCache *cache = nullptr;
+    std::chrono::steady_clock::time_point retry_after{};  // after a failed creation
+  };
   static std::mutex mu;
-  static std::map<int, FilterCache *> *caches = new std::map<int, FilterCache *>;  // kept until exit
+  static std::map<int, Slot> *caches = new std::map<int, Slot>;  // kept until exit
   std::lock_guard<std::mutex> g(mu);
-  FilterCache *&c = (*caches)[bits_per_key];
-  if (c && c->status() != OK) {  // an arena that could not be created is retried, not kept
-    delete c;
-    c = nullptr;
-  }
-  if (!c) {
-    uint64_t bytes = 1ull << 30;
-    if (const char *e = getenv("ADL_BLOOM_READER_CACHE_BYTES")) bytes = strtoull(e, nullptr, 10);
-    // less free device memory (other processes on the GPU): a quarter, then a sixteenth
-    for (int i = 0; i < 3; ++i, bytes /= 4) {
-      c = new FilterCache(bytes, 1u << 20, bits_per_key);
-      if (c->status() == OK) break;
-      delete c;
-      c = nullptr;
+  Slot &s = (*caches)[bits_per_key];
+  if (s.cache) return s.cache;  // only created (OK) caches are stored
+  // A failed creation is not retried on every reader open (each try holds this
+  // lock over up to three arena allocations): not again for a second.
+  const auto now = std::chrono::steady_clock::now();
+  if (now < s.retry_after) return nullptr;
+  const char *e = getenv("ADL_BLOOM_READER_CACHE_BYTES");
+  uint64_t bytes = e ? strtoull(e, nullptr, 10) : (1ull << 30);
+  // the default size shrinks when device memory is short (other processes on
+  // the GPU): a quarter, then a sixteenth; a size the user set is taken as is
+  const int tries = e ? 1 : 3;
+  for (int i = 0; i < tries; ++i, bytes /= 4) {
+    FilterCache *c = new FilterCache(bytes, 1u << 20, bits_per_key);
+    if (c->status() == OK) {
+      s.cache = c;
+      return c;
     }
+    delete c;
   }
-  return c;
+  s.retry_after = now + std::chrono::seconds(1);
+  return nullptr;
 }
 
 // ------------------------------------------------------------- FilterBlockReader

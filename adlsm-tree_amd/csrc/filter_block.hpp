@@ -47,6 +47,18 @@ class KeyArena {
     bytes_.reserve(bytes_.size() + bytes);
     offsets_.reserve(offsets_.size() + keys);
   }
+  /* keys i < n = base[off[i] .. off[i+1] - trim): a packed run of records
+   * whose last `trim` bytes are not part of the key (inner keys' seq + op);
+   * every record must be at least `trim` bytes.  Space is reserved once. */
+  void AddTrimmed(const char *base, const uint64_t *off, size_t n, size_t trim) {
+    if (!n) return;
+    bytes_.reserve(bytes_.size() + (size_t)(off[n] - off[0]) - n * trim);
+    offsets_.reserve(offsets_.size() + n);
+    for (size_t i = 0; i < n; ++i) {
+      bytes_.append(base + off[i], (size_t)(off[i + 1] - off[i]) - trim);
+      offsets_.push_back(bytes_.size());
+    }
+  }
   void Clear() {
     bytes_.clear();
     offsets_.assign(1, 0);
@@ -113,6 +125,8 @@ class FilterBlockWriter {
  public:
   explicit FilterBlockWriter(unique_ptr<FilterAlgorithm> &&method);
   RC Update(string_view key);
+  /* Update for a packed run (KeyArena::AddTrimmed): n keys, one reservation */
+  RC UpdateBatch(const char *base, const uint64_t *off, size_t n, size_t trim);
   RC Final(string &result);
   RC Keys2Block();
 

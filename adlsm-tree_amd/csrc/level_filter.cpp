@@ -141,8 +141,39 @@ void LevelCandidates(const vector<TableRange> &tables, const vector<string_view>
     const bool gone_at_max = Less(mx[t], Decoded{mx[t].user, seq, 0});
     (gone_at_max ? out_pt : out_gap)[at(mx[t].user)].push_back((uint32_t)t);
   }
+  vector<uint8_t> gone(T, 0);
+  for (size_t t = 0; t < T; ++t) gone[t] = !never[t] && Less(mx[t], Decoded{mx[t].user, seq, 0});
+  // The region lists hold sum(active tables per region) entries: for heavily
+  // overlapping tables (L0, wide ranges) that is O(T^2) whatever K is.  When it
+  // would exceed the K x T range tests of a direct scan, scan directly (the
+  // same predicate, in the same visiting order).
+  uint64_t total = 0;
+  {
+    int64_t active = 0;
+    for (size_t i = 0; i < NB; ++i) {
+      total += (uint64_t)active;  // the gap before B[i]
+      active += (int64_t)ins[i].size() - (int64_t)out_pt[i].size();
+      total += (uint64_t)active;  // B[i]
+      active -= (int64_t)out_gap[i].size();
+    }
+    total += (uint64_t)active;
+  }
+  if (total > (uint64_t)K * T) {
+    auto covers = [&](uint32_t t, string_view u) {
+      if (never[t] || u < mn[t].user) return false;
+      return u < mx[t].user || (u == mx[t].user && !gone[t]);
+    };
+    for (size_t i = 0; i < K; ++i) {
+      for (size_t r = T; r-- > 0;)
+        if (covers(asc[r], user_keys[i])) table.push_back(asc[r]);
+      begin[i + 1] = (uint32_t)table.size();
+    }
+    return;
+  }
   // region r: 2i = the gap before B[i], 2i+1 = B[i], 2*NB = the gap after the last
-  vector<uint32_t> rbeg(2 * NB + 2, 0), rlist;
+  vector<uint64_t> rbeg(2 * NB + 2, 0);
+  vector<uint32_t> rlist;
+  rlist.reserve(total);
   constexpr uint32_t kNil = ~0u;
   vector<uint32_t> nxt(T, kNil), prv(T, kNil);
   uint32_t head = kNil;
@@ -153,7 +184,7 @@ void LevelCandidates(const vector<TableRange> &tables, const vector<string_view>
   };
   auto record = [&](size_t r) {
     for (uint32_t t = head; t != kNil; t = nxt[t]) rlist.push_back(t);
-    rbeg[r + 1] = (uint32_t)rlist.size();
+    rbeg[r + 1] = rlist.size();
   };
   for (size_t i = 0; i < NB; ++i) {
     record(2 * i);  // the gap before B[i]

@@ -453,8 +453,10 @@ __global__ __launch_bounds__(kBlk) void pb_bin_kernel(const uint2 *__restrict__ 
   const int tid = threadIdx.x;
   const uint32_t total_chunks = scal[1];
   const uint32_t G = gridDim.x;
-  // the answers round 1 left (round 2), loaded with the hashes
+  // the answers round 1 left (round 2), loaded with the hashes; answers are one
+  // "cleared" bit per slot (1: a tested bit was clear, the answer is 0)
   const bool filt = round == 2;
+  uint32_t *clrw = reinterpret_cast<uint32_t *>(res);
   auto fetch = [&](uint32_t c, uint2 (&h)[kCPT], uint8_t (&al)[kCPT]) {
     if (c >= total_chunks) return;
     const uint32_t f = chunk_filter[c];
@@ -465,7 +467,7 @@ __global__ __launch_bounds__(kBlk) void pb_bin_kernel(const uint2 *__restrict__ 
     for (uint32_t r = 0; r < kCPT; ++r) {
       const uint32_t q = q0 + min(tid + r * kBlk, cnt - 1u);
       h[r] = hs[q];
-      al[r] = filt ? res[q] : (uint8_t)1;
+      al[r] = filt ? (uint8_t)(((clrw[q >> 5] >> (q & 31)) & 1u) ^ 1u) : (uint8_t)1;
     }
   };
   uint2 nxt[kCPT];
@@ -486,11 +488,12 @@ __global__ __launch_bounds__(kBlk) void pb_bin_kernel(const uint2 *__restrict__ 
     const FastMod mod{d.m, d.magic, d.shift, 0u};
     __syncthreads();  // the previous chunk's entries are read out of lpos
     for (uint32_t t = tid; t <= T; t += kBlk) hist[t] = 0;
+    // the chunk's cleared bits start at 0 (the words it shares with its
+    // neighbours are zeroed by both, before any pb_tile)
+    if (!filt && cnt)
+      for (uint32_t wd = (q0 >> 5) + tid; wd <= ((q0 + cnt - 1u) >> 5); wd += kBlk) clrw[wd] = 0u;
 #pragma unroll
-    for (uint32_t r = 0; r < kCPT; ++r) {
-      if (!filt && tid + r * kBlk < cnt) res[q0 + tid + r * kBlk] = 1;
-      live[r] = live[r] && tid + r * kBlk < cnt;
-    }
+    for (uint32_t r = 0; r < kCPT; ++r) live[r] = live[r] && tid + r * kBlk < cnt;
     __syncthreads();
     uint32_t pos[kCPT][KR];
 #pragma unroll
@@ -548,7 +551,7 @@ __global__ __launch_bounds__(kBlk) void pb_bin_kernel(const uint2 *__restrict__ 
 // registers at the tile's start and keeps two runs' loads in flight.
 constexpr uint32_t kTileVecPT = kTileBytes / 16 / kBlk;  // 16-byte tile vectors per thread
 constexpr int kRunLoads = 6;                             // entries per run per stage: 6 x 64 (runs average ~320)
-constexpr uint32_t kZRing = 256;                         // per-wave ring of answers to zero (128 when F > 3071)
+constexpr uint32_t kMaskWords = (kMaxC + 31) / 32 + 1;   // a wave's cleared-bit mask of one chunk (+ its shift)
 
 struct TileRef {
   uint32_t f, t, sh, nvec, tail;
@@ -588,31 +591,29 @@ __global__ __launch_bounds__(kBlk) void pb_tile_kernel(const uint8_t *__restrict
   uint32_t *ltile = lds;  // the tile's bitmap bytes from a 16-byte-aligned start (+ <= 15 bytes before it)
   uint32_t *ltb = lds + (kTileBytes + 64) / 4;  // the filters' first tiles (F+1), for the tile -> filter search
   const int tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid / kWave;
-  // A clear bit zeroes its query's answer.  Stores count with the run loads
-  // in vmcnt, in issue order, so a store issued between two stages of loads
-  // makes the wait for the later stage wait for the store too.  So each wave
-  // collects the answer indices of its clear bits in a private LDS ring and
-  // stores them after the tile's last run (64 per store instruction); only a
-  // ring that is nearly full flushes earlier.
-  const uint32_t zring = F + 1 <= 3072 ? kZRing : kZRing / 2, zmask = zring - 1;
-  uint32_t *zbuf = lds + (kTileBytes + 64) / 4 + ((F + 1 + 3) & ~3u) + (uint32_t)wave * zring;
-  uint32_t zhead = 0, zcnt = 0;  // wave-uniform
-  auto zflush64 = [&]() {
-    // this wave's LDS writes are done before its reads below (in order)
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    if ((uint32_t)lane < zcnt) res[zbuf[(zhead + lane) & zmask]] = 0;
-    const uint32_t done = zcnt < (uint32_t)kWave ? zcnt : (uint32_t)kWave;
-    zhead = (zhead + done) & zmask;
-    zcnt -= done;
-  };
-  auto zero_answer = [&](bool clr, uint32_t idx) {
-    const uint64_t m = __ballot(clr);
-    if (m == 0) return;
-    const uint32_t before = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-    if (clr) zbuf[(zhead + zcnt + before) & zmask] = idx;
-    zcnt += (uint32_t)__popcll(m);
-    if (zcnt > zring - (uint32_t)kWave) zflush64();  // room for the next 64
+  // A clear bit sets its query's "cleared" bit.  Each wave gathers the bits
+  // of the run (one chunk) it is testing in a private LDS mask of the chunk's
+  // 4 096 slots (shifted by the chunk's first slot mod 32), and ORs the mask's
+  // nonzero words into the global bit array with coalesced device-scope
+  // atomics when it moves to its next run: about 129 word atomics per run
+  // instead of ~1 200 scattered byte stores.  The flush is issued after a
+  // stage's tests and before the next stage's loads, so only the wait for the
+  // stage already in flight can include it.
+  uint32_t *clrw = reinterpret_cast<uint32_t *>(res);
+  uint32_t *zmaskw = lds + (kTileBytes + 64) / 4 + ((F + 1 + 3) & ~3u) + (uint32_t)wave * kMaskWords;
+  for (uint32_t w = (uint32_t)lane; w < kMaskWords; w += kWave) zmaskw[w] = 0u;
+  auto flush_run = [&](uint32_t rq) {
+#pragma unroll
+    for (uint32_t k2 = 0; k2 < 3; ++k2) {
+      const uint32_t w = (uint32_t)lane + k2 * kWave;
+      if (w < kMaskWords) {
+        const uint32_t v = zmaskw[w];
+        if (v) {
+          atomicOr(&clrw[(rq >> 5) + w], v);
+          zmaskw[w] = 0u;
+        }
+      }
+    }
   };
   constexpr int NW = kBlk / kWave;
   const uint32_t total_tiles = scal[0];
@@ -700,8 +701,9 @@ __global__ __launch_bounds__(kBlk) void pb_tile_kernel(const uint8_t *__restrict
     // all kRunLoads LDS words are read before any is tested (the reads are
     // unconditional -- a lane past the stage holds a clamped entry -- so they
     // issue back to back), then the clear bits go to the zero ring
-    auto consume = [&](const Stage &sg) {
+    auto consume = [&](const Stage &sg, const Stage &nx) {
       const uint32_t rq = d.qbase + sg.jc * C;  // the chunk's first answer (n < 2^31)
+      const uint32_t rs = rq & 31u;
       uint32_t w[kRunLoads];
 #pragma unroll
       for (int u = 0; u < kRunLoads; ++u) w[u] = ltile[((sg.x[u] & ((1u << kTL) - 1u)) + now.sh) >> 5];
@@ -710,8 +712,13 @@ __global__ __launch_bounds__(kBlk) void pb_tile_kernel(const uint8_t *__restrict
         const uint32_t bit = (sg.x[u] & ((1u << kTL) - 1u)) + now.sh;
         // bitwise, not short-circuit: no branch per entry
         const bool clr = (sg.b0 + u * kWave + lane < sg.b1) & (((w[u] >> (bit & 31)) & 1u) == 0u) & !(exp & 1);
-        zero_answer(clr, rq + (sg.x[u] >> kTL));
+        if (clr) {
+          const uint32_t b = rs + (sg.x[u] >> kTL);
+          atomicOr(&zmaskw[b >> 5], 1u << (b & 31));
+        }
       }
+      // the run ends here: the next stage is another run's, or past the last
+      if (sg.live && (!nx.live || nx.jc != sg.jc)) flush_run(rq);
     };
     for (uint32_t q0 = 0; q0 < nq; q0 += kWave) {
       const uint32_t nr = min((uint32_t)kWave, nq - q0);
@@ -745,12 +752,11 @@ __global__ __launch_bounds__(kBlk) void pb_tile_kernel(const uint8_t *__restrict
       take(A);
       while (A.live) {
         take(B);
-        consume(A);
+        consume(A, B);
         take(A);
-        consume(B);
+        consume(B, A);
       }
     }
-    while (zcnt) zflush64();  // this tile's answers, after its last run
   }
 }
 
@@ -792,7 +798,9 @@ __global__ __launch_bounds__(kBlk) void pb_gather_kernel(const uint16_t *__restr
     src[r] = lstart[lo] + (pl - lbase[lo]);
   }
 #pragma unroll
-  for (uint32_t r = 0; r < kQPT; ++r) v[r] = nvalid ? res[src[r]] : (uint8_t)0;
+  for (uint32_t r = 0; r < kQPT; ++r)
+    v[r] = nvalid ? (uint8_t)(((reinterpret_cast<const uint32_t *>(res)[src[r] >> 5] >> (src[r] & 31)) & 1u) ^ 1u)
+                  : (uint8_t)0;
 #pragma unroll
   for (uint32_t r = 0; r < kQPT; ++r)
     if (tid + r * kBlk >= nvalid) v[r] = 0;
@@ -862,13 +870,18 @@ int adl_bloom_probe_batch_device(const uint8_t *d_keys, const uint64_t *d_offset
   const size_t lds_k6 = (size_t)(kQB / 4 + 3 * (F + 1) + 32) * 4;      // answers + 3 per-filter arrays + scratch
   const size_t lds_p1 = (size_t)(kMaxTiles + 4 + 64 + p.k * p.C) * 4;
   const size_t lds_p2 = (size_t)kTileBytes + 64 + (size_t)((F + 1 + 3) & ~3u) * 4 +
-                        (size_t)(kBlk / kWave) * (F + 1 <= 3072 ? kZRing : kZRing / 2) * 4;
+                        (size_t)(kBlk / kWave) * kMaskWords * 4;
   try {
     hipLaunchKernelGGL(pb_desc_kernel, dim3(1), dim3(kBlk), 0, st, d_bitmap_off, d_bitmap_end, F, desc, scal);
     ADL_HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(pb_hist_kernel, dim3(p.nb), dim3(kBlk), lds_k1, st, d_filter_id, n, F, p.nb, desc, cnt);
     ADL_HIP_TRY(hipGetLastError());
-    if (getenv("ADL_PB_OLDSCAN")) {  // round-2 K2 (tuning A/B)
+#ifdef ADL_BLOOM_STAMPS
+    const bool old_scan = getenv("ADL_PB_OLDSCAN") != nullptr;  // diagnostics build: round-2 K2 (A/B)
+#else
+    constexpr bool old_scan = false;
+#endif
+    if (old_scan) {
       hipLaunchKernelGGL(pb_rows_kernel, dim3(F + 1), dim3(256), 0, st, cnt, p.nb, F, desc);
       ADL_HIP_TRY(hipGetLastError());
       hipLaunchKernelGGL(pb_scan_kernel, dim3(F + 1), dim3(kBlk), 0, st, cnt, start, p.nb, F, p.C, p.maxch, desc, cf,
@@ -884,16 +897,22 @@ int adl_bloom_probe_batch_device(const uint8_t *d_keys, const uint64_t *d_offset
       ADL_HIP_TRY(hipGetLastError());
     }
     if (int rc = adl_host::lds_limit<pb_scatter_kernel>()) return rc;
+#ifdef ADL_BLOOM_STAMPS
     const char *exp_env = getenv("ADL_PB_EXP");  // diagnostics build only
     const uint32_t exp = exp_env ? (uint32_t)atoi(exp_env) : 0u;
+#else
+    constexpr uint32_t exp = 0;
+#endif
     hipLaunchKernelGGL(pb_scatter_kernel, dim3(p.nb), dim3(kBlk), lds_k3, st, reinterpret_cast<const uint4 *>(d_keys),
                        d_filter_id, n, F, p.nb, desc, cnt, start, dest, hs, exp);
     ADL_HIP_TRY(hipGetLastError());
     // k = 6: two rounds, bits 0 .. split-1 of every query, then the rest for
     // the queries still answered 1 (ADL_PB_SPLIT = 0: one round of all k)
+    // (a tuning knob read per call so tests can flip it; a value other than
+    // 0, 1, 2 is ignored)
     const char *split_env = getenv("ADL_PB_SPLIT");
-    const uint32_t split = p.k == 6 ? (split_env ? (uint32_t)atoi(split_env) : kSplit6) : 0u;
-    if (split > 2) return ADL_ERR_INVALID_ARG;
+    uint32_t split = split_env ? (uint32_t)atoi(split_env) : kSplit6;
+    if (p.k != 6 || split > 2) split = p.k == 6 ? kSplit6 : 0u;
     if (int rc = adl_host::lds_limit<pb_tile_kernel>()) return rc;
     using BinK = decltype(&pb_bin_kernel<6>);
     auto bin = [&](BinK kern, int lds_rc, uint32_t j0, uint32_t round) -> int {

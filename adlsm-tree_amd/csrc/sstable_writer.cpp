@@ -12,6 +12,13 @@
 
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
+#include <deque>
+#include <functional>
+#include <mutex>
+#include <thread>
+
+#include "../../include/adl_bloom.h"
 
 namespace adl {
 
@@ -164,13 +171,27 @@ RC SSTableWriter::Add(string_view inner_key, string_view value) {
   return OK;
 }
 
+/* A packed sorted run (memtable flush, src/mem_table.cpp:96-105; MergeRuns
+ * output, src/db.cpp:428-509): the user keys go into the filter arena in one
+ * bulk append (one reservation, no per-entry call), then the entries into the
+ * data blocks.  Same bytes as Add() per entry; every record is checked before
+ * anything is added, so a BAD_RECORD leaves the writer unchanged. */
 RC SSTableWriter::AddBatch(const char *keys, const uint64_t *key_off, const char *values,
                            const uint64_t *val_off, size_t n) {
+  if (filter_job_.valid()) return BAD_RECORD;
+  for (size_t i = 0; i < n; ++i)
+    if (key_off[i + 1] < key_off[i] || key_off[i + 1] - key_off[i] < 9) return BAD_RECORD;
+  filter_block_.UpdateBatch(keys, key_off, n, 9);
   for (size_t i = 0; i < n; ++i) {
-    RC rc = Add(string_view(keys + key_off[i], key_off[i + 1] - key_off[i]),
-                string_view(values + val_off[i], val_off[i + 1] - val_off[i]));
+    const string_view k(keys + key_off[i], key_off[i + 1] - key_off[i]);
+    RC rc = data_block_.Add(k, string_view(values + val_off[i], val_off[i + 1] - val_off[i]));
     if (rc) return rc;
+    if (data_block_.EstimatedSize() > need_flush_size_) {
+      last_key_.assign(k.data(), k.size());
+      if ((rc = FlushDataBlock())) return rc;
+    }
   }
+  if (n) last_key_.assign(keys + key_off[n - 1], key_off[n] - key_off[n - 1]);
   return OK;
 }
 
@@ -192,31 +213,101 @@ RC SSTableWriter::FlushDataBlock() {
   return index_block_.Add(last_key_, handle);
 }
 
+// ------------------------------------------------------------ filter worker
+/* One worker thread per calling thread, created by its first BeginFinal and
+ * joined when that thread exits: the filter builds of consecutive tables run
+ * on one thread, so the library's per-thread staging buffers, streams and
+ * device workspace are allocated once, not per table.  Each job first makes
+ * the caller's HIP device current (a thread starts on device 0). */
+class FilterWorker {
+ public:
+  FilterWorker() : th_([this] { Run(); }) {}
+  ~FilterWorker() {
+    {
+      lock_guard<mutex> g(mu_);
+      stop_ = true;
+    }
+    cv_.notify_one();
+    th_.join();
+  }
+  future<FilterOutcome> Post(function<FilterOutcome()> job) {
+    packaged_task<FilterOutcome()> task(std::move(job));
+    future<FilterOutcome> f = task.get_future();
+    {
+      lock_guard<mutex> g(mu_);
+      q_.push_back(std::move(task));
+    }
+    cv_.notify_one();
+    return f;
+  }
+  static FilterWorker &ForThisThread() {
+    thread_local unique_ptr<FilterWorker> w;
+    if (!w) w = make_unique<FilterWorker>();
+    return *w;
+  }
+
+ private:
+  void Run() {
+    for (;;) {
+      packaged_task<FilterOutcome()> task;
+      {
+        unique_lock<mutex> g(mu_);
+        cv_.wait(g, [this] { return stop_ || !q_.empty(); });
+        if (q_.empty()) return;  // stop_, and every posted build has run
+        task = std::move(q_.front());
+        q_.pop_front();
+      }
+      task();
+    }
+  }
+  mutex mu_;
+  condition_variable cv_;
+  deque<packaged_task<FilterOutcome()>> q_;
+  bool stop_ = false;
+  thread th_;
+};
+
 /* src/sstable.cpp:54-99: data tail, filter block (GPU build), meta block
- * ("filter" -> handle), index block, footer; the oid is the SHA-256 of it all. */
+ * ("filter" -> handle), index block, footer; the oid is the SHA-256 of it all.
+ * Final builds the filter on the calling thread (its HIP device, its
+ * adl_bloom_profile_enable timing). */
 RC SSTableWriter::Final(unsigned char sha256_digit[32]) {
-  if (RC rc = BeginFinal()) return rc;
-  return EndFinal(sha256_digit);
+  if (filter_job_.valid()) return BAD_RECORD;
+  RC rc;
+  if (!data_block_.Empty() && (rc = FlushDataBlock())) return rc;
+  const auto f0 = std::chrono::steady_clock::now();
+  rc = filter_block_.Final(filter_out_);  // the reference drops this RC
+  filter_seconds_ = std::chrono::duration<double>(std::chrono::steady_clock::now() - f0).count();
+  if (rc) return rc;
+  return WriteTail(sha256_digit);
 }
 
 RC SSTableWriter::BeginFinal() {
   if (filter_job_.valid()) return BAD_RECORD;
   RC rc;
   if (!data_block_.Empty() && (rc = FlushDataBlock())) return rc;
+  int32_t dev = 0;
+  if (adl_bloom_get_device(&dev) != ADL_OK) return DEVICE_ERROR;
   // the worker owns filter_block_ and filter_out_ until EndFinal's get()
-  filter_job_ = std::async(std::launch::async, [this] {
+  filter_job_ = FilterWorker::ForThisThread().Post([this, dev]() -> FilterOutcome {
+    if (adl_bloom_set_device(dev) != ADL_OK) return {DEVICE_ERROR, 0.0};
     const auto f0 = std::chrono::steady_clock::now();
-    const RC r = filter_block_.Final(filter_out_);  // the reference drops this RC
-    filter_seconds_ = std::chrono::duration<double>(std::chrono::steady_clock::now() - f0).count();
-    return r;
+    const RC r = filter_block_.Final(filter_out_);
+    return {r, std::chrono::duration<double>(std::chrono::steady_clock::now() - f0).count()};
   });
   return OK;
 }
 
 RC SSTableWriter::EndFinal(unsigned char sha256_digit[32]) {
   if (!filter_job_.valid()) return BAD_RECORD;
-  RC rc = filter_job_.get();
-  if (rc) return rc;
+  const FilterOutcome out = filter_job_.get();
+  filter_seconds_ = out.seconds;
+  if (out.rc) return out.rc;
+  return WriteTail(sha256_digit);
+}
+
+RC SSTableWriter::WriteTail(unsigned char sha256_digit[32]) {
+  RC rc;
   buffer_ = std::move(filter_out_);
   if ((rc = Emit(buffer_))) return rc;
   filter_block_handle_.SetMeta(offset_, (int)buffer_.size());

@@ -127,6 +127,12 @@ class PosixFileSink : public Sink {
   int fd_ = -1;
 };
 
+/* what a filter build hands back to EndFinal */
+struct FilterOutcome {
+  RC rc;
+  double seconds;
+};
+
 /* src/sstable.hpp:21-71 */
 class SSTableWriter {
  public:
@@ -141,22 +147,25 @@ class SSTableWriter {
   RC AddBatch(const char *keys, const uint64_t *key_off, const char *values, const uint64_t *val_off,
               size_t n);
   RC Final(unsigned char sha256_digit[32]);
-  /* Final() in two halves (Final == BeginFinal + EndFinal), so a caller that
-   * writes several tables -- a compaction's outputs, src/db.cpp:428-509 --
-   * can fill the next table while this one's filter builds on the GPU.
-   * BeginFinal flushes the data tail and starts the filter build on a worker
-   * thread; EndFinal waits for it and writes the filter, meta, index and
+  /* Final() in two halves, so a caller that writes several tables -- a
+   * compaction's outputs, src/db.cpp:428-509 -- can fill the next table while
+   * this one's filter builds on the GPU.  BeginFinal flushes the data tail and
+   * hands the filter build to the calling thread's filter worker (one
+   * persistent thread per calling thread, running on the caller's current HIP
+   * device); EndFinal waits for it and writes the filter, meta, index and
    * footer blocks.  No Add between the two (BAD_RECORD); the file and its oid
-   * are the same as Final's. */
+   * are the same as Final's.  Final itself builds on the calling thread. */
   RC BeginFinal();
   RC EndFinal(unsigned char sha256_digit[32]);
   int GetFileSize() const { return offset_; }
-  /* wall time of the filter block build inside the last Final() */
+  /* wall time of the filter block build of the last Final() / EndFinal();
+   * not valid between BeginFinal and EndFinal */
   double filter_seconds() const { return filter_seconds_; }
 
  private:
   RC FlushDataBlock();
   RC Emit(const string &block);
+  RC WriteTail(unsigned char sha256_digit[32]);
 
   Sink *sink_;
   int offset_ = 0;
@@ -171,7 +180,7 @@ class SSTableWriter {
   /* BeginFinal's build and its block (declared in this order so the future,
    * whose destructor waits for the build, goes first) */
   string filter_out_;
-  future<RC> filter_job_;
+  future<FilterOutcome> filter_job_;
   static constexpr size_t need_flush_size_ = 1u << 12; /* 4KB, src/sstable.hpp:40 */
 };
 

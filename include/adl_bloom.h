@@ -301,6 +301,12 @@ int adl_bloom_murmur3_device(const uint8_t *d_keys, const uint64_t *d_offsets, u
  * computed on the GPU.  Synchronous; on failure *h_out is left untouched. */
 int adl_bloom_murmur3(uint32_t seed, const void *data, uint64_t len, uint32_t *h_out);
 
+/* The calling thread's current HIP device (every device pointer above belongs
+ * to it), and setting it: for host code that hands a build to another thread
+ * (SSTableWriter::BeginFinal's worker), whose current device starts at 0. */
+int adl_bloom_get_device(int32_t *device);
+int adl_bloom_set_device(int32_t device);
+
 /* ---------------------------------------------------------------- instrumentation */
 
 /* Per-kernel timing of the build for the calling thread: while enabled, each

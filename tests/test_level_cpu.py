@@ -71,6 +71,26 @@ def test_level_candidates_vs_oracle(lvl, oracle, seed):
         assert got[i] == oracle.level_candidates(tables, k, seq), (i, k)
 
 
+@pytest.mark.parametrize("seed,K", [(0, 1), (1, 3), (2, 40), (3, 400)])
+def test_level_candidates_overlapping_direct_scan(lvl, oracle, seed, K):
+    """An L0-shaped level: 300 tables whose ranges nearly all overlap, so the
+    region lists would hold O(T^2) entries; with few lookups LevelCandidates
+    scans the tables directly instead (same predicate, same visiting order).
+    K = 400 takes the region sweep again; both must equal the oracle."""
+    rng = np.random.default_rng(100 + seed)
+    users = sorted({b"u%05d" % int(x) for x in rng.integers(0, 5000, 600)})
+    tables = []
+    for _ in range(300):
+        a = int(rng.integers(0, 40))
+        b = int(rng.integers(len(users) - 40, len(users)))
+        tables.append((inner(users[a], int(rng.integers(0, 50)), 1), inner(users[b], int(rng.integers(0, 50)), 1)))
+    keys = [users[int(i)] for i in rng.integers(0, len(users), K)]
+    seq = 25
+    got = candidates(lvl, tables, keys, seq)
+    for i, k in enumerate(keys):
+        assert got[i] == oracle.level_candidates(tables, k, seq), (i, k)
+
+
 def test_level_candidates_disjoint_level_scales(lvl, oracle):
     """An L1-shaped level (disjoint ranges, 2 000 tables) and 20 000 lookups:
     at most one candidate each, the right one."""
