@@ -7,7 +7,18 @@ no collective on its data path: one process per GPU, and torch.distributed
 throughput counters.  The probe does have a real exchange step: a query must
 reach the GPU that holds its table's filter, and its answer must come back to
 the rank that asked (bucket queries by owner, stable, and
-scatter the results back).  route_probe does that with two all-to-alls.
+scatter the results back).
+
+Two forms of that step:
+  * owner-bucketed (bench.py's measured path at N > 1): the host buckets the
+    batch by owner once, before upload (owner_select), so each rank is handed
+    exactly its own tables' queries and probes them with no collective at all;
+    the answers are put back in the batch's order afterwards (scatter_answers,
+    outside the timed loop).  This is the LSM's natural case: a lookup is
+    issued where its level's tables live.
+  * routed (route_probe): every rank holds an arbitrary slice of the batch and
+    two all-to-alls per step move queries to their owners and answers back;
+    bench.py reports it as roofline.routing_variant.
 """
 from __future__ import annotations
 
@@ -121,3 +132,37 @@ def route_probe(keys, fid, owner, local_id, probe_fn, group=None, comm_cpu=None,
     out = torch.empty(keys.shape[0], dtype=torch.uint8, device=dev)
     out[order] = back(a_back)
     return out, int(sum(recv))
+
+
+def owner_select(fid, owner, local_id, rank: int):
+    """Owner-bucketed batch: the positions (ascending, so the batch order is
+    kept) of the queries whose table `rank` owns, and their filter ids local
+    to that rank.  fid: global table ids (torch tensor); owner / local_id:
+    per-table tensors (owner_table) on fid's device."""
+    import torch
+
+    f = fid.long()
+    idx = torch.nonzero(owner[f] == rank).squeeze(1)
+    return idx, local_id[f[idx]].to(torch.int32)
+
+
+def scatter_answers(ans, idx, total: int, group=None):
+    """Inverse of owner_select over all ranks: every rank's answers `ans` (uint8)
+    at batch positions `idx` into one (total,) uint8 tensor in batch order, on
+    every rank.  Each position is answered by exactly one rank, so a SUM
+    all-reduce of the zero-filled per-rank vectors assembles it (host tensors
+    for gloo)."""
+    import torch
+    import torch.distributed as dist
+
+    dev = ans.device
+    full = torch.zeros(total, dtype=torch.uint8, device=dev)
+    full[idx] = ans.to(torch.uint8)
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
+        return full
+    if dist.get_backend(group) == "gloo":
+        host = full.to("cpu", torch.int32)
+        dist.all_reduce(host, op=dist.ReduceOp.SUM, group=group)
+        return host.to(torch.uint8).to(dev)
+    dist.all_reduce(full, op=dist.ReduceOp.SUM, group=group)
+    return full

@@ -13,14 +13,19 @@ pass A (hash + bin) and pass B (LDS tile OR + bitmap write).  Workloads:
               (strong scaling: the 256 tables are fixed).
   varlen      10M variable-length keys (8-256 B, Zipf(1.1) lengths) per GPU (configs[2]).
   probe       100M 16 B queries against 256 device-resident 1M-key filters (configs[4]);
-              filters t -> GPU t // (256/N); rank r asks queries [r*Q/N, (r+1)*Q/N) of the
-              stream, which travel to their filter's GPU and back (RCCL all-to-all,
-              adlbloom.dist.route_probe) -- strong scaling, the 100M total is fixed.
+              filters t -> GPU t // (256/N).  At N > 1 the batch is bucketed by owner
+              before upload, so each GPU is handed exactly its own
+              tables' queries: no collective on the data path; strong scaling, the
+              100M total is fixed.  The routed form (every rank asks a slice of the
+              batch; two RCCL all-to-alls per step, adlbloom.dist.route_probe) is
+              timed after it and reported as roofline.routing_variant.
 
-Multi-GPU: one process per GPU (torch.distributed.run).  The builds have no
-collective on the data path -- each rank owns whole filters; the probe's
-query routing is its one exchange step.  RCCL also reduces the key counter
-(sum) and the elapsed time (max).  Rank 0 prints one JSON line.
+Multi-GPU: one process per GPU (torch.distributed.run).  No workload has a
+collective on its data path -- each rank owns whole filters.  RCCL reduces the
+key counter (sum) and the elapsed time (max).  The default workload also
+reports configs[3] as a `compaction_strong` sub-record (256 tables split over
+the N GPUs, strong scaling), the north star's multi-GPU target.  Rank 0
+prints one JSON line.
 """
 import argparse
 import hashlib
@@ -53,6 +58,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget")
+    ap.add_argument("--no-compaction-strong", action="store_true",
+                    help="single: skip the configs[3] compaction_strong sub-record")
     return ap.parse_args()
 
 
@@ -144,9 +151,34 @@ class Workload:
         self.local_id = torch.from_numpy(lid).cuda()
         if queries % world:
             raise SystemExit(f"--queries {queries} must divide over {world} ranks")
-        self.q0, self.n = rank * (queries // world), queries // world
-        self.keys, self.fid, self.member = ab.synth_probe_queries(self.n, q0=self.q0, num_tables=PROBE_TABLES,
-                                                                  keys_per_table=per)
+        self.gidx = None  # batch positions of this rank's queries (owner-bucketed, N > 1)
+        if world == 1:
+            self.n = queries
+            self.keys, self.fid, self.member = ab.synth_probe_queries(queries, num_tables=PROBE_TABLES,
+                                                                      keys_per_table=per)
+        else:
+            # owner-bucketed: the whole batch, bucketed by owner before
+            # upload -- this rank keeps exactly its own tables' queries, batch order kept;
+            # self.fid holds filter ids local to this rank
+            ks, fs, ms, ix = [], [], [], []
+            chunk = 8_000_000
+            for q0 in range(0, queries, chunk):
+                k, f, m = ab.synth_probe_queries(min(chunk, queries - q0), q0=q0, num_tables=PROBE_TABLES,
+                                                 keys_per_table=per)
+                idx, lf = D.owner_select(f, self.owner, self.local_id, rank)
+                ks.append(k[idx])
+                fs.append(lf)
+                ms.append(m[idx])
+                ix.append(idx + q0)
+                del k, f, m
+            self.keys, self.fid, self.member, self.gidx = (torch.cat(ks), torch.cat(fs), torch.cat(ms),
+                                                           torch.cat(ix))
+            self.n = int(self.keys.shape[0])
+            # the routed variant's input: this rank's contiguous slice of the batch
+            rq0, rn = rank * (queries // world), queries // world
+            self.route_n = rn
+            self.route_keys, self.route_fid, _ = ab.synth_probe_queries(rn, q0=rq0, num_tables=PROBE_TABLES,
+                                                                        keys_per_table=per)
         self.total_queries = queries
         self.bytes_per_launch = ALGO_BYTES_PER_QUERY * self.n
         self.kernel_events = []  # (start, stop) of every probe launch
@@ -157,7 +189,8 @@ class Workload:
                        "queries_total": queries, "queries_this_gpu": self.n, "filters_total": PROBE_TABLES,
                        "filters_per_gpu": len(tables), "keys_per_filter": per, "bits_per_key": BPK,
                        "routing": "none (one GPU)" if world == 1 else
-                       "RCCL all-to-all of queries to their filter's GPU and of answers back, inside each step"}
+                       "owner-bucketed: each GPU is handed its own tables' queries (bucketed by owner before "
+                       "upload); no collective on the data path"}
         self.dtype = "u32"
 
     def _probe_local(self, keys, lfid):
@@ -176,21 +209,26 @@ class Workload:
 
     def step(self):
         if self.kind == "probe":
-            if self.world == 1:
-                return self._probe_local(self.keys, self.fid)
-            from adlbloom import dist as D
-
-            st = {}
-            out, self.served = D.route_probe(self.keys, self.fid, self.owner, self.local_id, self._probe_local,
-                                             stats=st)
-            # DESIGN.md §6's cost model: (N-1)/N of the queries cross xGMI, 20 B out and 1 B back
-            self.routing = dict(st, bytes_per_query_out=D.ROUTE_BYTES_OUT, bytes_per_query_back=D.ROUTE_BYTES_BACK,
-                                offrank_fraction=round(st["queries_sent_offrank"] / max(self.n, 1), 4),
-                                model_offrank_fraction=round((self.world - 1) / self.world, 4))
-            return out
+            return self._probe_local(self.keys, self.fid)
         if self.kind == "varlen":
             return self.builder.build(self.keys, self.offs)
         return self.builder.build(self.keys)
+
+    def step_routed(self):
+        """The routed probe (N > 1): this rank's slice of the batch goes to the
+        tables' owners and the answers come back, two RCCL all-to-alls."""
+        import adlbloom as ab
+        from adlbloom import dist as D
+
+        st = {}
+        out, _ = D.route_probe(self.route_keys, self.route_fid, self.owner, self.local_id,
+                               lambda k, f: ab.probe_batch(k, f, self.bitmaps, self.bitmap_off), stats=st)
+        # DESIGN.md §6's cost model: (N-1)/N of the queries cross xGMI, 20 B out and 1 B back
+        self.routing = dict(st, bytes_per_query_out=D.ROUTE_BYTES_OUT, bytes_per_query_back=D.ROUTE_BYTES_BACK,
+                            offrank_fraction=round(st["queries_sent_offrank"] / max(self.route_n, 1), 4),
+                            model_offrank_fraction=round((self.world - 1) / self.world, 4))
+        return out
+
 
 
 def _cpu_cores():
@@ -302,8 +340,13 @@ def probe_check(w, out, rank, world):
     exit, counted on a sample of rank 0's queries to its own filters."""
     import numpy as np
 
-    allout = gather_all(out, world)
-    allmem = gather_all(w.member, world)
+    if world > 1:  # owner-bucketed: every rank's answers back in batch order
+        from adlbloom import dist as D
+
+        allout = D.scatter_answers(out, w.gidx, w.total_queries)
+        allmem = D.scatter_answers(w.member, w.gidx, w.total_queries)
+    else:
+        allout, allmem = out, w.member
     if rank != 0:
         return None
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -321,22 +364,21 @@ def probe_check(w, out, rank, world):
         sha = hashlib.sha256(allout.cpu().numpy().tobytes()).hexdigest()
         rec["oracle"] = ("all %dM answers bit-identical to the oracle (sha256)" % (w.total_queries // 1_000_000)
                          if sha == pins["probe"]["results_sha256"] else f"MISMATCH sha256 {sha}")
-    else:  # no pin for this batch: rank 0's first 200K queries to its own filters against the oracle
-        fid0 = w.fid.cpu().numpy().astype(np.int64)
-        sel0 = np.nonzero((fid0 >= w.tables.start) & (fid0 < w.tables.stop))[0][:200_000]
-        want = O.probe_multi(w.keys.cpu().numpy()[sel0], (fid0[sel0] - w.tables.start).astype(np.uint32),
+    else:  # no pin for this batch: rank 0's first 200K queries (all to its own filters) against the oracle
+        sel0 = np.arange(min(w.n, 200_000))
+        want = O.probe_multi(w.keys[:sel0.size].cpu().numpy(), w.fid[:sel0.size].cpu().numpy().astype(np.uint32),
                              w.bitmaps.cpu().numpy(), np.asarray(w.bitmap_off_host, dtype=np.uint64),
                              bits_per_key=BPK)
-        got = out.cpu().numpy()[sel0]
+        got = out[:sel0.size].cpu().numpy()
         rec["oracle"] = ("parity unpinned (no pin for this batch); %d sampled answers identical to the oracle"
                          % sel0.size if np.array_equal(got, want) else "MISMATCH on sampled answers")
-    # reads per query on rank 0's own filters
+    # reads per query on rank 0's own filters (w.fid: filter ids local to this rank)
     fid_all = w.fid.cpu().numpy().astype(np.int64)
-    sel = np.nonzero((fid_all >= w.tables.start) & (fid_all < w.tables.stop))[0][:200_000]
+    sel = np.arange(min(w.n, 200_000))
     bms = w.bitmaps.cpu().numpy()
     off = np.asarray(w.bitmap_off_host, dtype=np.int64)
-    h = O.murmur3_batch(w.keys.cpu().numpy()[sel])
-    lf = fid_all[sel] - w.tables.start
+    h = O.murmur3_batch(w.keys[:sel.size].cpu().numpy())
+    lf = fid_all[sel]
     base = off[lf]
     m = (off[lf + 1] - base) * 8
     alive = np.ones(sel.size, dtype=bool)
@@ -651,6 +693,27 @@ def main():
 
     total_keys, elapsed_max = D.reduce_throughput(float(w.n) * args.steps, elapsed, device="cuda")
 
+    def timed(fn, steps, warmup=2):
+        """max over ranks of the wall time of `steps` calls, barriers on both sides"""
+        for _ in range(warmup):
+            fn()
+        barrier()
+        t = time.perf_counter()
+        for _ in range(steps):
+            fn()
+        barrier()
+        return D.reduce_throughput(0.0, time.perf_counter() - t, device="cuda")[1]
+
+    # the routed probe (N > 1), reported beside the owner-bucketed measurement
+    routing_variant = None
+    if probe and world > 1:
+        el = timed(w.step_routed, args.steps)
+        routing_variant = {
+            "form": "routed: every GPU asks a contiguous slice of the batch; each step sends every query to its "
+                    "table's GPU and the answer back (2 RCCL all-to-alls, adlbloom.dist.route_probe)",
+            "value": round(w.total_queries * args.steps / el / 1e6, 1), "unit": "Mqueries/s",
+            "ms_per_step": round(el / max(args.steps, 1) * 1e3, 4), "rank0_traffic": w.routing}
+
     parity = None
     if rank == 0 and args.workload == "single":
         parity = parity_check(out, w.n, w.keys)
@@ -658,6 +721,22 @@ def main():
         parity = probe_check(w, out, rank, world)
     else:
         parity = build_parity(w, rank)
+
+    # configs[3] beside the headline: the north star's multi-GPU target (256
+    # tables split over the N GPUs, strong scaling), its own clock
+    comp_strong = None
+    if args.workload == "single" and not args.no_compaction_strong:
+        wc = Workload("compaction", rank, 0, world)
+        el = timed(wc.step, args.steps)
+        tot = D.reduce_throughput(float(wc.n) * args.steps, 0.0, device="cuda")[0]
+        comp_strong = {"metric": "Mkeys/s bloom-filter build (device-resident), 16B keys, bits/key=10, "
+                                 "configs[3]: 256 SSTables x 1M keys split over the GPUs",
+                       "value": round(tot / el / 1e6, 1), "unit": "Mkeys/s",
+                       "ms_per_step": round(el / max(args.steps, 1) * 1e3, 4), "steps": args.steps,
+                       "scaling": "strong", "tables_total": COMPACTION_TABLES, "tables_per_gpu": len(wc.tables),
+                       "parity": build_parity(wc, rank)}
+        del wc
+        torch.cuda.empty_cache()
 
     if rank == 0:
         if probe:
@@ -749,8 +828,10 @@ def main():
                 "positions": pos, "per_key": round(pos / w.n, 3),
                 "round_trip_bytes": 8 * pos,  # 4 B written by pass A, read by pass B
                 "note": "k bit-sets per key, less the keys whose hash pair their workgroup had already counted"}
-        if probe and world > 1:
-            out_json["roofline"]["routing"] = w.routing
+        if routing_variant:
+            out_json["roofline"]["routing_variant"] = routing_variant
+        if comp_strong:
+            out_json["compaction_strong"] = comp_strong
         if world == 1 and args.workload == "single" and not args.no_e2e:
             out_json["e2e"] = e2e(w.n)
         if world == 1 and args.workload == "compaction" and not args.no_e2e:

@@ -161,3 +161,64 @@ def test_two_ranks_gloo_probe_routing_matches_single_process():
     assert np.array_equal(got, want)
     assert sum(o[2] for o in out) == Q  # every query probed exactly once, by its table's owner
     assert got[m.astype(bool)].all()
+
+
+def _owner_worker(rank, world, port, q):
+    """Owner-bucketed probe over gloo (bench.py's measured path at N > 1): the
+    whole configs[4] batch (scaled down) is bucketed by owner before upload,
+    each rank probes only its own tables' queries -- no collective on the data
+    path -- and scatter_answers puts every answer back in batch order."""
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "adlsm-tree_amd"))
+    sys.path.insert(0, os.path.join(root, "oracle"))
+    import torch
+    import torch.distributed as dist
+
+    from adlbloom import dist as D
+    import oracle as O
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        T, per, Q = 16, 3000, 20000
+        tables = D.table_shard(T, world, rank)
+        bms = [O.keys2block(O.splitmix_keys16(0x5EED + t, per)) for t in tables]
+        arena = np.concatenate(bms)
+        off = np.concatenate([[0], np.cumsum([b.size for b in bms])]).astype(np.uint64)
+        own, lid = D.owner_table(T, world)
+        k, f, m = O.synth_probe_queries(Q, num_tables=T, keys_per_table=per)
+        idx, lf = D.owner_select(torch.from_numpy(f.astype(np.int64)), torch.from_numpy(own),
+                                 torch.from_numpy(lid), rank)
+        assert np.all(np.diff(idx.numpy()) > 0)  # batch order kept
+        assert np.all(own[f[idx.numpy()]] == rank)
+        ans = torch.from_numpy(O.probe_multi(k[idx.numpy()], lf.numpy().astype(np.uint32), arena, off))
+        full = D.scatter_answers(ans, idx, Q)
+        q.put((rank, full.numpy().tobytes(), int(idx.numel())))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_ranks_gloo_owner_bucketed_probe_matches_single_process():
+    import torch.multiprocessing as mp
+
+    import oracle as O
+
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_owner_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = sorted(q.get(timeout=180) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    T, per, Q = 16, 3000, 20000
+    bms = [O.keys2block(O.splitmix_keys16(0x5EED + t, per)) for t in range(T)]
+    off = np.concatenate([[0], np.cumsum([b.size for b in bms])]).astype(np.uint64)
+    k, f, m = O.synth_probe_queries(Q, num_tables=T, keys_per_table=per)
+    want = O.probe_multi(k, f, np.concatenate(bms), off)
+    for _, full, _ in out:  # every rank holds all answers in batch order
+        assert np.array_equal(np.frombuffer(full, dtype=np.uint8), want)
+    assert sum(o[2] for o in out) == Q  # each query probed once, by its table's owner

@@ -6,9 +6,12 @@ RCCL run is the driver's).  SURVEY.md §8e:
   adlbloom.dist.table_shard, each rank one segmented build of its share;
   every table of both ranks against the oracle's SHA-256
   (tests/golden/full_size.json);
-* probe -- configs[4]'s 100M queries, rank r asking [r*50M, (r+1)*50M),
-  routed to the rank owning each query's filter and back
-  (adlbloom.dist.route_probe, two all-to-alls); the 100M answers, gathered in
+* probe -- configs[4]'s 100M queries, both forms of bench.py's N > 1 probe:
+  owner-bucketed (the measured path: the batch bucketed by owner before
+  upload, each rank probing only its own tables' queries, the answers put back
+  in batch order by adlbloom.dist.scatter_answers) and routed (rank r asking
+  [r*50M, (r+1)*50M), sent to the rank owning each query's filter and back by
+  adlbloom.dist.route_probe, two all-to-alls); the 100M answers of each, in
   query order, against the oracle's SHA-256.
 """
 import json
@@ -50,14 +53,23 @@ def _worker(rank, world, port, q):
                       for i in range(len(w.tables))]
         del w
         torch.cuda.empty_cache()
+        from adlbloom import dist as D
+
         p = bench.Workload("probe", rank, 0, world, 100_000_000)
         out = p.step()
-        out = p.step()  # twice: routing state does not leak between steps
+        out = p.step()  # twice: nothing leaks between steps
         torch.cuda.synchronize()
         res["served"] = p.served
-        allout = bench.gather_all(out, world)
+        allout = D.scatter_answers(out, p.gidx, 100_000_000)
         if rank == 0:
             res["probe_sha"] = hashlib.sha256(allout.cpu().numpy().tobytes()).hexdigest()
+        del allout
+        out = p.step_routed()
+        out = p.step_routed()  # routing state does not leak between steps
+        torch.cuda.synchronize()
+        allout = bench.gather_all(out, world)
+        if rank == 0:
+            res["routed_sha"] = hashlib.sha256(allout.cpu().numpy().tobytes()).hexdigest()
         q.put((rank, res))
     except Exception as e:  # report, do not hang the other rank's test
         q.put((rank, {"error": repr(e)}))
@@ -90,3 +102,4 @@ def test_two_ranks_one_gpu_compaction_and_probe_routing():
             assert sha == want[t], (r, t)
     assert out[0]["served"] + out[1]["served"] == 100_000_000
     assert out[0]["probe_sha"] == pins["probe"]["results_sha256"]
+    assert out[0]["routed_sha"] == pins["probe"]["results_sha256"]

@@ -1,17 +1,17 @@
 #!/bin/bash
-# tools/r03_final.sh -- round-3 evidence in one GPU call: PMC passes (traffic +
+# tools/final.sh -- one round's evidence in one GPU call: PMC passes (traffic +
 # integer issue) written into profiles/pmc_traffic.json first (bench.py reads
 # them), the GPU test suite, smoke(), the read-path latency bench, every bench
 # workload with CPU baselines, and rocprofv3 kernel traces of the headline and
 # var-len runs.
 set -u
 cd "$(dirname "$0")/.."
-OUT=gpurun_out/${TAG:-r03f}
+OUT=gpurun_out/${TAG:?set TAG, e.g. TAG=r04a}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 step() { echo "=== $1 ($(date +%T))"; }
 step pmc
-bash tools/r03_pmc.sh "$OUT/pmc" single varlen compaction probe > "$OUT/pmc.log" 2>&1 || { tail -5 "$OUT/pmc.log"; exit 1; }
+bash tools/pmc_all.sh "$OUT/pmc" single varlen compaction probe > "$OUT/pmc.log" 2>&1 || { tail -5 "$OUT/pmc.log"; exit 1; }
 step pytest
 timeout -k 10 900 python -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -n 4 "$OUT/pytest_gpu.log"; [ $rc -ne 0 ] && exit $rc

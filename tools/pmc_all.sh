@@ -1,8 +1,8 @@
 #!/bin/bash
-# tools/r03_pmc.sh -- PMC passes per workload into profiles/pmc_traffic.json:
+# tools/pmc_all.sh -- PMC passes per workload into profiles/pmc_traffic.json:
 # FETCH_SIZE, WRITE_SIZE (traffic; tools/pmc_traffic.py) and the integer-issue
 # group (tools/pmc_alu.py).  Each pass its own rocprofv3 run (tools/pmc.sh).
-# usage: bash tools/r03_pmc.sh OUTDIR workload...
+# usage: bash tools/pmc_all.sh OUTDIR workload...
 set -u
 cd "$(dirname "$0")/.."
 OUT=$1; shift
