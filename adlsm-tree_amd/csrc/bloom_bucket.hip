@@ -58,7 +58,7 @@ constexpr uint32_t kWaves = kBlock / kWave;     // 16
 constexpr uint32_t kTL = 20;                    // log2 bits per tile: 128 KiB of LDS in pass B
 constexpr uint32_t kTileWords = 1u << (kTL - 5);
 constexpr uint32_t kTMask = (1u << kTL) - 1u;
-constexpr uint32_t kRing = 32;                  // bucket slots per tile, pass A
+constexpr uint32_t kRingMin = 32, kRingMax = 1024;  // bucket slots per tile, pass A (a power of two)
 constexpr uint32_t kGran = 16;                  // entries per flushed granule (64 B)
 constexpr uint32_t kMaxTiles = 1024;            // flush owners: 64 lanes x 16 waves
 constexpr uint32_t kListCap = 2 * kWave;        // flush-list entries per wave (<= 2 granules per owner)
@@ -91,9 +91,9 @@ static_assert(sizeof(BkDesc) % 16 == 0, "descriptors load as whole uint4s");
 struct BkArgs {
   uint32_t nf, k, total_slices, total_tiles;
   uint32_t tmax;       // pass A LDS tile rows (max T, multiple of 4)
+  uint32_t ring;       // pass A bucket slots per tile (power of two, 32 .. 1024)
   uint32_t dd_log2;    // pass A: slots (log2) of the table that skips keys whose h1 == h2 repeats (0: off)
   uint32_t nt_bitmap;  // pass B: non-temporal bitmap stores
-  uint32_t pad_;
   BkDesc f[kMaxFilt];
 };
 
@@ -150,26 +150,77 @@ __global__ __launch_bounds__(256) void bk_fill_maps_kernel(const BkDesc *__restr
   for (uint32_t i = threadIdx.x; i < d.T; i += 256) tile_f[d.tile0 + i] = f;
 }
 
+// ---------------------------------------------------------------- diagnostics
+// -DADL_BLOOM_STAMPS only (make stamps): wave 0 of every workgroup sums
+// s_memtime cycles per phase; adl_bloom_debug_stamps appends them after the
+// chunk/table build's (tools/stamps.py BK=1).  The product library has none.
+#ifdef ADL_BLOOM_STAMPS
+__device__ uint64_t g_bk_stamps[2][256][16][8];  // pass A, pass B; workgroup < 256, every wave
+#define BK_STAMP_DECL                                  \
+  uint64_t bst_acc_[8] = {0, 0, 0, 0, 0, 0, 0, 0}; \
+  uint64_t bst_t_ = __builtin_amdgcn_s_memtime();
+#define BK_STAMP(i)                                    \
+  do {                                                 \
+    const uint64_t t_ = __builtin_amdgcn_s_memtime(); \
+    bst_acc_[i] += t_ - bst_t_;                        \
+    bst_t_ = t_;                                       \
+  } while (0)
+#define BK_STAMP_FLUSH(pass)                                                                          \
+  do {                                                                                                \
+    if ((threadIdx.x & 63) == 0 && blockIdx.x < 256)                                                  \
+      for (int i_ = 0; i_ < 8; ++i_) g_bk_stamps[pass][blockIdx.x][threadIdx.x / 64][i_] = bst_acc_[i_]; \
+  } while (0)
+#else
+#define BK_STAMP_DECL
+#define BK_STAMP(i) do { } while (0)
+#define BK_STAMP_FLUSH(pass) do { } while (0)
+#endif
+
 // Ring slot -> LDS word of tile t's bucket.  The XOR moves whole aligned
 // 4-word groups (bits 2..4 of the slot), so a 16-entry granule is still four
 // aligned 16-byte groups, while buckets of different tiles start on
 // different banks.
-__device__ __forceinline__ uint32_t ring_word(uint32_t t, uint32_t slot) {
-  return t * kRing + (slot ^ ((t & 7u) << 2));
+__device__ __forceinline__ uint32_t ring_word(uint32_t t, uint32_t slot, uint32_t lgS) {
+  return (t << lgS) + (slot ^ ((t & 7u) << 2));
 }
 
 // ---------------------------------------------------------------- pass A
 // K > 0: k known at compile time (positions and claims unrolled); K == 0:
 // runtime k (a.k), one position at a time.
-template <int K, bool DT>
-__global__ __launch_bounds__(kBlock) void bk_bin16_kernel(BkArgs a, const uint4 *__restrict__ keys,
+// Key sources: 16-byte keys (hashed here), or the (h1, h2) pairs the
+// var-len hashing pass wrote (bloom_build.hip, hash_var_kernel), indexed like
+// the keys relative to the group's first key.
+struct BkSrc16 {
+  const uint4 *keys;
+  using Raw = uint4;
+  __device__ __forceinline__ Raw load(uint64_t i) const { return load_nt(keys + i); }
+  __device__ static __forceinline__ void hash(const Raw &r, uint32_t &h1, uint32_t &h2) { hash16(r, h1, h2); }
+};
+typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
+struct BkSrcPairs {
+  const uint2 *pairs;
+  using Raw = uint2;
+  __device__ __forceinline__ Raw load(uint64_t i) const {
+    const u32x2_t v = __builtin_nontemporal_load(reinterpret_cast<const u32x2_t *>(pairs + i));
+    return make_uint2(v.x, v.y);
+  }
+  __device__ static __forceinline__ void hash(const Raw &r, uint32_t &h1, uint32_t &h2) {
+    h1 = r.x;
+    h2 = r.y;
+  }
+};
+
+template <int K, class Src, bool DT>
+__global__ __launch_bounds__(kBlock) void bk_bin16_kernel(BkArgs a, Src src,
                                                           uint32_t *__restrict__ ws, BkTable ft) {
   using F = BF<DT>;
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   const uint32_t tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid / kWave;
   const uint32_t TM = a.tmax;
-  uint32_t *ring = lds;                  // TM x kRing positions
-  uint32_t *word = ring + TM * kRing;    // per tile: (ring start << 16) | entries claimed since the last flush
+  const uint32_t S = a.ring;             // slots per tile bucket (a power of two >= 32)
+  const uint32_t lgS = 31u - __clz(S);
+  uint32_t *ring = lds;                  // TM x S positions
+  uint32_t *word = ring + TM * S;        // per tile: (ring start << 16) | entries claimed since the last flush
   uint32_t *flg = word + TM;             // per tile: granules copied out
   uint32_t *cur = flg + TM;              // per tile: current overflow extent (slice-area word offset)
   uint2 *wl = reinterpret_cast<uint2 *>(cur + TM) + wave * kListCap;  // this wave's flush list
@@ -179,10 +230,14 @@ __global__ __launch_bounds__(kBlock) void bk_bin16_kernel(BkArgs a, const uint4 
   // "any thread has work left", one word per batch parity (__syncthreads_or
   // would take static LDS of its own, past the 160 KiB this kernel declares)
   uint32_t *more_flag = bump + 1;
+  // a word per lane that a rejected claim writes instead of the ring (the
+  // claim phase stores unconditionally); nothing reads it
+  uint32_t *sink = bump + 4 + lane;
   const uint32_t kk = K > 0 ? (uint32_t)K : a.k;
   const uint32_t all = kk >= 32 ? ~0u : (1u << kk) - 1u;
 
   int fprev = -1;
+  BK_STAMP_DECL
   for (uint32_t s = blockIdx.x; s < a.total_slices; s += gridDim.x) {
     const int fi = F::of_slice(a, ft, s);
     const auto &d = F::at(a, ft, fi);
@@ -205,6 +260,7 @@ __global__ __launch_bounds__(kBlock) void bk_bin16_kernel(BkArgs a, const uint4 
     }
     fprev = fi;
     __syncthreads();
+    BK_STAMP(5);  // slice set-up
 
     // Copy every full granule out (FINAL: every entry, the last granule
     // partial) -- owner lane `lane` of wave `wave` owns tile wave*tpw + lane.
@@ -221,15 +277,13 @@ __global__ __launch_bounds__(kBlock) void bk_bin16_kernel(BkArgs a, const uint4 
       if (own) {
         const uint32_t w = word[t];
         start = w >> 16;
-        f = min(w & 0xffffu, kRing);
+        f = min(w & 0xffffu, S);
         g = FINAL ? (f + kGran - 1) / kGran : f / kGran;
         fl = flg[t];
       }
-      const uint64_t b0 = __ballot(g & 1u), b1 = __ballot((g >> 1) & 1u);
-      const uint32_t pre = __builtin_amdgcn_mbcnt_hi((uint32_t)(b0 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b0, 0u)) +
-                           2u * __builtin_amdgcn_mbcnt_hi((uint32_t)(b1 >> 32),
-                                                          __builtin_amdgcn_mbcnt_lo((uint32_t)b1, 0u));
-      const uint32_t tot = (uint32_t)__popcll(b0) + 2u * (uint32_t)__popcll(b1);
+      const uint32_t incl = wave_incl_scan(g, (int)lane);
+      const uint32_t pre = incl - g;
+      const uint32_t tot = __builtin_amdgcn_readlane(incl, kWave - 1);
       if (own) {
         for (uint32_t i = 0; i < g; ++i) {
           const uint32_t e = (fl + i) * kGran;  // entry offset in the (slice, tile) stream
@@ -245,12 +299,12 @@ __global__ __launch_bounds__(kBlock) void bk_bin16_kernel(BkArgs a, const uint4 
             }
             tgt = cur[t] + o;
           }
-          wl[pre + i] = make_uint2(t | (((start + i * kGran) & (kRing - 1)) << 16), tgt);
+          wl[pre + i] = make_uint2(t | (((start + i * kGran) & (S - 1)) << 16), tgt);
         }
         if (FINAL) {
           ws[d.count_base + (uint64_t)t * d.R + sl] = fl * kGran + f;
         } else {
-          word[t] = (((start + g * kGran) & (kRing - 1)) << 16) | (f - g * kGran);
+          word[t] = (((start + g * kGran) & (S - 1)) << 16) | (f - g * kGran);
           flg[t] = fl + g;
         }
       }
@@ -259,75 +313,134 @@ __global__ __launch_bounds__(kBlock) void bk_bin16_kernel(BkArgs a, const uint4 
         if (e < tot) {
           const uint2 le = wl[e];
           const uint32_t tt = le.x & 0xffffu, ro = le.x >> 16, q = lane & 3u;
-          const uint4 v = *reinterpret_cast<const uint4 *>(ring + ring_word(tt, ro + 4u * q));
+          const uint4 v = *reinterpret_cast<const uint4 *>(ring + ring_word(tt, ro + 4u * q, lgS));
           *reinterpret_cast<uint4 *>(area + le.y + 4u * q) = v;
         }
       }
     };
 
-    const uint4 *kp = keys + d.key_begin + first;
+    const uint64_t kp = d.key_begin + first;
     const uint32_t last = cnt ? cnt - 1u : 0u;
     uint32_t j = 0;     // keys this thread has taken
-    uint32_t pend = 0;  // positions of the current key still to place
-    uint32_t h1 = 0, h2 = 0;
-    uint4 nxt = make_uint4(0, 0, 0, 0);
-    if (cnt) nxt = load_nt(kp + min(tid, last));
-    for (uint32_t it = 0;; ++it) {
-      if (pend == 0 && tid + j * kBlock < cnt) {
-        hash16(nxt, h1, h2);
+    // Two keys per thread in flight: A is being placed (its positions'
+    // claims), B is hashed while A's claims are in flight, so the murmur VALU
+    // overlaps the LDS atomics across the waves of a SIMD instead of running
+    // in a phase of its own.  A claim rejected by a full bucket keeps its bit
+    // in pendA and is retried next batch; B then waits.
+    constexpr int KP = K > 0 ? K : 1;
+    uint32_t posA[KP], posB[KP];
+    uint32_t pendA = 0, pendB = 0;
+    bool hasB = false;
+    uint32_t h1 = 0, h2 = 0;  // K == 0: the hashes of A
+    uint32_t h1B = 0, h2B = 0;
+    typename Src::Raw nxt{};
+    if (cnt) nxt = src.load(kp + min(tid, last));
+    // Hash the loaded key into B and load the one after it.
+    auto take = [&]() {
+      if (!hasB && tid + j * kBlock < cnt) {
+        Src::hash(nxt, h1B, h2B);
         ++j;
-        pend = all;
+        hasB = true;
+        pendB = all;
         // the reference's murmur variant collapses: 39 % of SplitMix keys have
         // h1 == h2, on few values; a key whose h1 == h2 value this workgroup
         // already placed (same filter) sets no new bit.  Skipped only when the
         // slot holds exactly its value, installed by a key that was placed.
-        if (dd && h1 == h2) {
-          const uint32_t old = atomicCAS(&dtab[h1 >> (32u - dd)], ~0u, h1);
-          if (old != ~0u && old == h1) pend = 0;
+        if (dd && h1B == h2B) {
+          const uint32_t old = atomicCAS(&dtab[h1B >> (32u - dd)], ~0u, h1B);
+          if (old != ~0u && old == h1B) pendB = 0;
         }
-        if (cnt) nxt = load_nt(kp + min(tid + j * kBlock, last));
+        if (cnt) nxt = src.load(kp + min(tid + j * kBlock, last));
+        if (K > 0) {
+#pragma unroll
+          for (int jj = 0; jj < KP; ++jj) posB[jj] = fastmod(h1B + (uint32_t)jj * h2B, mod);
+        }
       }
-      if (K > 0) {
-        uint32_t pos[K > 0 ? K : 1], old[K > 0 ? K : 1];
+    };
+    auto promote = [&]() {  // B becomes A once A is placed
+      if (pendA == 0 && hasB) {
 #pragma unroll
-        for (int jj = 0; jj < K; ++jj) pos[jj] = fastmod(h1 + (uint32_t)jj * h2, mod);
+        for (int jj = 0; jj < KP; ++jj) posA[jj] = posB[jj];
+        pendA = pendB;
+        h1 = h1B;
+        h2 = h2B;
+        hasB = false;
+      }
+    };
+    take();
+    promote();
+    for (uint32_t it = 0;; ++it) {
+      // Typical wave: every lane's key A has all k positions or none left (a
+      // retried claim is rare), so one exec mask covers the k claims and the
+      // writes go out unconditionally (a rejected one into the lane's sink).
+      const bool whole = (pendA == 0 || pendA == all);
+      if (K > 0 && __all(whole)) {
+        uint32_t old[KP];
+        if (pendA) {
 #pragma unroll
-        for (int jj = 0; jj < K; ++jj)
-          old[jj] = ((pend >> jj) & 1u) ? atomicAdd(&word[pos[jj] >> kTL], 1u) : 0xffffu;
+          for (int jj = 0; jj < KP; ++jj) old[jj] = atomicAdd(&word[posA[jj] >> kTL], 1u);
+        }
+        take();  // hash the next key while the atomics are in flight
+        if (pendA) {
+          uint32_t left = 0;
 #pragma unroll
-        for (int jj = 0; jj < K; ++jj) {
+          for (int jj = 0; jj < KP; ++jj) {
+            const uint32_t rel = old[jj] & 0xffffu;
+            const uint32_t t = posA[jj] >> kTL;
+            uint32_t *dst = ring + ring_word(t, ((old[jj] >> 16) + rel) & (S - 1), lgS);
+            *(rel < S ? dst : sink) = posA[jj];
+            left |= rel < S ? 0u : 1u << jj;
+          }
+          pendA = left;
+        }
+      } else if (K > 0) {
+        uint32_t old[KP];
+#pragma unroll
+        for (int jj = 0; jj < KP; ++jj)
+          old[jj] = ((pendA >> jj) & 1u) ? atomicAdd(&word[posA[jj] >> kTL], 1u) : 0xffffu;
+        take();
+#pragma unroll
+        for (int jj = 0; jj < KP; ++jj) {
           const uint32_t rel = old[jj] & 0xffffu;
-          if (rel < kRing) {
-            const uint32_t t = pos[jj] >> kTL;
-            ring[ring_word(t, ((old[jj] >> 16) + rel) & (kRing - 1))] = pos[jj];
-            pend &= ~(1u << jj);
+          if (rel < S) {
+            const uint32_t t = posA[jj] >> kTL;
+            ring[ring_word(t, ((old[jj] >> 16) + rel) & (S - 1), lgS)] = posA[jj];
+            pendA &= ~(1u << jj);
           }
         }
       } else {
         for (uint32_t jj = 0; jj < kk; ++jj) {
-          if ((pend >> jj) & 1u) {
+          if ((pendA >> jj) & 1u) {
             const uint32_t p = fastmod(h1 + jj * h2, mod);
             const uint32_t t = p >> kTL;
             const uint32_t o = atomicAdd(&word[t], 1u), rel = o & 0xffffu;
-            if (rel < kRing) {
-              ring[ring_word(t, ((o >> 16) + rel) & (kRing - 1))] = p;
-              pend &= ~(1u << jj);
+            if (rel < S) {
+              ring[ring_word(t, ((o >> 16) + rel) & (S - 1), lgS)] = p;
+              pendA &= ~(1u << jj);
             }
           }
         }
+        take();
       }
+      promote();
+      BK_STAMP(0);  // claims + hash of the next key
       __syncthreads();  // claims and writes of this batch complete
+      BK_STAMP(1);  // claim barrier
       flush(std::false_type{});
-      if (pend != 0 || tid + j * kBlock < cnt) more_flag[it & 1u] = 1u;
+      BK_STAMP(2);  // flush
+      if (pendA != 0 || hasB || tid + j * kBlock < cnt) more_flag[it & 1u] = 1u;
       __syncthreads();  // also: the flush has read the ring before new claims
       const bool any = more_flag[it & 1u] != 0;
       // the other word is next written after the next batch's claim barrier
       if (tid == 0) more_flag[(it + 1u) & 1u] = 0;
+      BK_STAMP(3);  // end barrier
       if (!any) break;
     }
     flush(std::true_type{});
     __syncthreads();  // LDS reused by the next slice
+    BK_STAMP(4);  // final flush
   }
+  BK_STAMP_FLUSH(0);
 }
 
 // ---------------------------------------------------------------- pass B
@@ -346,18 +459,30 @@ __global__ __launch_bounds__(kBlock) void bk_tile_kernel(BkArgs a, const uint32_
   uint32_t *cfast = pre + kMaxSlices;        // entries in the slice's region (<= cap)
   uint32_t *cfull = cfast + kMaxSlices;      // all entries
   uint32_t *scratch = cfull + kMaxSlices;    // block scan (kWaves + 1)
+  uint32_t *ovf = scratch + kWaves + 1;      // some slice of this tile overflowed its region
+  if (tid == 0) *ovf = 0;
   {
     uint4 *t4 = reinterpret_cast<uint4 *>(tile);
     for (uint32_t i = tid; i < kTileWords / 4; i += kBlock) t4[i] = make_uint4(0, 0, 0, 0);
   }
+  BK_STAMP_DECL
+  // thread i's slice count of a tile, loaded one tile ahead (unconditionally,
+  // at a clamped index: an unconditional load keeps the gather's counted waits)
+  auto count_of = [&](uint32_t tg) -> uint32_t {
+    const auto &d = F::at(a, ft, F::of_tile(a, ft, tg));
+    const uint32_t R = d.R;
+    return ws[d.count_base + (uint64_t)(tg - d.tile0) * R + min(tid, R ? R - 1u : 0u)];
+  };
+  uint32_t c_next = blockIdx.x < a.total_tiles ? count_of(blockIdx.x) : 0u;
   for (uint32_t tg = blockIdx.x; tg < a.total_tiles; tg += gridDim.x) {
     const auto &d = F::at(a, ft, F::of_tile(a, ft, tg));
     const uint32_t t = tg - d.tile0, R = d.R, cap = d.cap, tstride = cap + kLink, stride = d.stride;
     const uint32_t *abase = ws + d.area_base;
     // (a count can never exceed the slice's k*L positions; clamped so that a
     // corrupted workspace gives a wrong bitmap, never a wild read or a long walk)
-    uint32_t c = 0;
-    if (tid < R) c = min(ws[d.count_base + (uint64_t)t * R + tid], a.k * d.L);
+    const uint32_t c = tid < R ? min(c_next, a.k * d.L) : 0u;
+    c_next = count_of(tg + gridDim.x < a.total_tiles ? tg + gridDim.x : tg);
+    if (c > cap) *ovf = 1;
     const uint32_t cf = min(c, cap);
     uint32_t U;
     const uint32_t ex = block_excl_scan<kBlock>((cf + kWave - 1) / kWave, scratch, &U);  // (barriers inside)
@@ -367,6 +492,7 @@ __global__ __launch_bounds__(kBlock) void bk_tile_kernel(BkArgs a, const uint32_
       cfull[tid] = c;
     }
     __syncthreads();
+    BK_STAMP(0);  // counts staged and scanned
 
     const uint32_t u0 = (uint32_t)(((uint64_t)U * wave) / kWaves);
     const uint32_t u1 = (uint32_t)(((uint64_t)U * (wave + 1)) / kWaves);
@@ -388,23 +514,24 @@ __global__ __launch_bounds__(kBlock) void bk_tile_kernel(BkArgs a, const uint32_
       }
       struct Stage {
         uint32_t v[D];
+        uint32_t val[D];  // valid entries of each slot's unit (wave-uniform)
       };
       // A stage's loads are issued unconditionally (a slot past nb reads
       // unit 0 again and is masked out), so the compiler waits vmcnt(D) for
-      // the older stage instead of vmcnt(0).
+      // the older stage instead of vmcnt(0).  Lanes past a unit's valid
+      // entries read the unit's first word, so they fetch no extra line.
       auto issue = [&](Stage &st, uint32_t q0) {
 #pragma unroll
         for (int u = 0; u < D; ++u) {
           const uint32_t i = min(q0 + (uint32_t)u, (uint32_t)kWave - 1u);
-          st.v[u] = abase[__builtin_amdgcn_readlane(doff, i) + lane];
+          st.val[u] = q0 + (uint32_t)u < nb ? __builtin_amdgcn_readlane(dval, i) : 0u;
+          st.v[u] = abase[__builtin_amdgcn_readlane(doff, i) + (lane < st.val[u] ? lane : 0u)];
         }
       };
-      auto consume = [&](const Stage &st, uint32_t q0) {
+      auto consume = [&](const Stage &st, uint32_t) {
 #pragma unroll
         for (int u = 0; u < D; ++u) {
-          const uint32_t i = q0 + (uint32_t)u;
-          const uint32_t val = i < nb ? __builtin_amdgcn_readlane(dval, min(i, (uint32_t)kWave - 1u)) : 0u;
-          if (lane < val) {
+          if (lane < st.val[u]) {
             const uint32_t off = st.v[u] & kTMask;
             atomicOr(&tile[off >> 5], 1u << (off & 31u));
           }
@@ -419,8 +546,9 @@ __global__ __launch_bounds__(kBlock) void bk_tile_kernel(BkArgs a, const uint32_
         consume(B, q0 + D);
       }
     }
+    BK_STAMP(1);  // gather + or (this wave's units)
     // entries past a region (skewed key sets only): follow the extent chain
-    for (uint32_t s = wave; s < R; s += kWaves) {
+    for (uint32_t s = wave; *ovf && s < R; s += kWaves) {
       const uint32_t cs = cfull[s];
       if (cs <= cap) continue;
       const uint32_t sb = s * stride;
@@ -439,7 +567,9 @@ __global__ __launch_bounds__(kBlock) void bk_tile_kernel(BkArgs a, const uint32_
         lk = sb + ext + d.xo;
       }
     }
+    BK_STAMP(2);  // overflow chains
     __syncthreads();  // the tile is complete
+    BK_STAMP(3);  // tile barrier
 
     // write the tile: bytes [t << (kTL-3), ...) of this filter, up to the
     // 16-byte-rounded bitmap length (pad bytes are zero: no position lands
@@ -449,6 +579,7 @@ __global__ __launch_bounds__(kBlock) void bk_tile_kernel(BkArgs a, const uint32_
     const uint32_t nvec = (uint32_t)(min(tile_bytes, (uint64_t)d.alloc_bytes - b0) >> 4);
     uint4 *out4 = reinterpret_cast<uint4 *>(bitmaps + d.bitmap_off + b0);
     uint4 *t4 = reinterpret_cast<uint4 *>(tile);
+    if (tid == 0) *ovf = 0;  // next set after the barrier below
     for (uint32_t i = tid; i < kTileWords / 4; i += kBlock) {
       const uint4 v = t4[i];
       t4[i] = make_uint4(0, 0, 0, 0);
@@ -458,7 +589,9 @@ __global__ __launch_bounds__(kBlock) void bk_tile_kernel(BkArgs a, const uint32_
       }
     }
     __syncthreads();  // read out and zero again; counts staged for the next tile
+    BK_STAMP(4);  // write + zero tile
   }
+  BK_STAMP_FLUSH(1);
 }
 
 // ---------------------------------------------------------------- host plan
@@ -467,11 +600,13 @@ struct BkPlan {
   std::vector<BkDesc> f;
   bool dt = false;
   uint64_t area_words = 0, count_words = 0, ft_bytes = 0, ws_bytes = 0;
+  uint64_t pair_off = 0, scratch_off = 0;  // var-len keys: (h1, h2) pairs, then the hashing pass's table
   uint32_t grid_a = 0, grid_b = 0;
+  uint32_t depth_b = 8;
   size_t lds_a = 0, lds_b = 0;
 };
 
-constexpr size_t kLdsB = (size_t)(kTileWords + 3 * kMaxSlices + kWaves + 1) * 4;
+constexpr size_t kLdsB = (size_t)(kTileWords + 3 * kMaxSlices + kWaves + 2) * 4;
 
 int make_plan(const uint64_t *counts, uint32_t nf, int32_t bpk, BkPlan &p) {
   if (nf == 0 || bpk < 0) return ADL_ERR_INVALID_ARG;
@@ -542,41 +677,63 @@ int make_plan(const uint64_t *counts, uint32_t nf, int32_t bpk, BkPlan &p) {
     tile += (uint32_t)T;
     tmax = std::max<uint32_t>(tmax, (uint32_t)T);
   }
+  const uint32_t tpw = (tmax + kWaves - 1) / kWaves;  // flush owners per wave
   tmax = (uint32_t)adl_host::round_up(tmax, 4);
-  // pass A LDS: rings + 3 words per tile, the flush lists, the pair table
-  const uint32_t fixed = 35 * tmax + 2 * kWaves * kListCap + 4;
-  if (fixed > kLdsWords) return ADL_ERR_TOO_LARGE;
+  // pass A LDS: TM x S ring slots and 3 words per tile, the flush lists, the
+  // pair table.  S: the largest power of two whose rings fit beside a
+  // 256-slot pair table and whose full flush (S/16 granules per owner) fits a
+  // wave's list; the pair table then takes what is left, up to 2^12 slots.
+  const uint32_t lists = 2 * kWaves * kListCap + 4 + kWave;  // + pool word, 2 flags, pad; the sink words
+  uint32_t S = 0;
+  for (uint32_t r = kRingMax; r >= kRingMin; r /= 2)
+    if (tmax * (r + 3) + lists + 256 <= kLdsWords && tpw * (r / kGran) <= kListCap) {
+      S = r;
+      break;
+    }
+  if (!S) return ADL_ERR_TOO_LARGE;
+  const uint32_t fixed = tmax * (S + 3) + lists;
   uint32_t dd = 0;
-  if (adl_host::env_on("ADL_BLOOM_HASH_DEDUP", true)) {
-    const uint32_t lg_max = std::min<uint32_t>(adl_host::env_on("ADL_BLOOM_BK_DD13", false) ? 13 : 12, 13);
-    for (uint32_t lg = lg_max; lg >= 8; --lg)
+  if (adl_host::env_on("ADL_BLOOM_HASH_DEDUP", true))
+    for (uint32_t lg = 12; lg >= 8; --lg)
       if (fixed + (1u << lg) <= kLdsWords) {
         dd = lg;
         break;
       }
-  }
   p.a.nf = nf;
   p.a.k = k;
   p.a.total_slices = slice;
   p.a.total_tiles = tile;
   p.a.tmax = tmax;
+  p.a.ring = S;
   p.a.dd_log2 = dd;
   p.a.nt_bitmap = adl_host::env_on("ADL_BLOOM_NT_BITMAP", true) ? 1u : 0u;
   p.area_words = adl_host::round_up(area, 64);
   p.count_words = adl_host::round_up(cntw + kPad, 64);
   for (BkDesc &d : p.f) d.count_base += p.area_words;  // the count tables follow the areas
   p.ft_bytes = p.dt ? adl_host::round_up(nf * sizeof(BkDesc), 256) + 4ull * (slice + tile) + 256 : 0;
-  p.ws_bytes = (p.area_words + p.count_words) * 4 + p.ft_bytes + 256;
+  // Every key shape is sized for (the workspace query does not carry it): var-len
+  // keys add their (h1, h2) pairs and, past kMaxFilt filters, the hashing pass's
+  // descriptor table (bloom_build.hip: at most 128 B per filter and one word
+  // per run of >= 256 keys).
+  p.pair_off = adl_host::round_up((p.area_words + p.count_words) * 4 + p.ft_bytes, 256);
+  p.scratch_off = p.pair_off + adl_host::round_up(8 * total_n + 16, 256);
+  const uint64_t scratch = nf > (uint32_t)kMaxFilt ? adl_host::round_up(128ull * nf, 256) + 4 * (total_n / 256 + nf + 1) + 512
+                                                   : 0;
+  p.ws_bytes = p.scratch_off + scratch + 256;
   p.lds_a = (size_t)(fixed + (dd ? (1u << dd) : 0u)) * 4;
   p.lds_b = kLdsB;
+  {
+    const char *e = getenv("ADL_BLOOM_BK_DEPTH");
+    p.depth_b = e ? (uint32_t)atoi(e) : 8u;
+  }
   p.grid_a = std::min<uint32_t>(slice, cus);
   p.grid_b = std::min<uint32_t>(tile, cus);
   if (!p.dt) std::copy(p.f.begin(), p.f.end(), p.a.f);
   return ADL_OK;
 }
 
-template <bool DT>
-int launch(BkPlan &p, const uint4 *keys, uint8_t *bitmaps, void *ws, hipStream_t st, hipEvent_t *ev) {
+template <bool DT, class Src>
+int launch(BkPlan &p, Src keys, uint8_t *bitmaps, void *ws, hipStream_t st, hipEvent_t *ev) {
   uint32_t *w = reinterpret_cast<uint32_t *>(ws);
   BkTable ft{};
   if constexpr (DT) {
@@ -599,18 +756,24 @@ int launch(BkPlan &p, const uint4 *keys, uint8_t *bitmaps, void *ws, hipStream_t
       ADL_HIP_TRY(hipGetLastError());
       return ADL_OK;
     };
-    const int rc = p.a.k == 6 ? go(adl_host::lds_limit<bk_bin16_kernel<6, DT>>, bk_bin16_kernel<6, DT>)
-                              : go(adl_host::lds_limit<bk_bin16_kernel<0, DT>>, bk_bin16_kernel<0, DT>);
+    const int rc = p.a.k == 6 ? go(adl_host::lds_limit<bk_bin16_kernel<6, Src, DT>>, bk_bin16_kernel<6, Src, DT>)
+                              : go(adl_host::lds_limit<bk_bin16_kernel<0, Src, DT>>, bk_bin16_kernel<0, Src, DT>);
     if (rc) return rc;
   } else if (ev) {  // no keys: an empty pass-A interval
-    ADL_HIP_TRY(hipEventRecord(ev[0], st));
-    ADL_HIP_TRY(hipEventRecord(ev[1], st));
+    if (ev[0]) ADL_HIP_TRY(hipEventRecord(ev[0], st));
+    if (ev[1]) ADL_HIP_TRY(hipEventRecord(ev[1], st));
   }
-  if (int rc = adl_host::lds_limit<bk_tile_kernel<8, DT>>()) return rc;
-  hipExtLaunchKernelGGL(bk_tile_kernel<8, DT>, dim3(p.grid_b), dim3(kBlock), p.lds_b, st, ev ? ev[2] : nullptr,
-                        ev ? ev[3] : nullptr, 0, p.a, (const uint32_t *)w, bitmaps, ft);
-  ADL_HIP_TRY(hipGetLastError());
-  return ADL_OK;
+  auto go_b = [&](auto lim, auto kern) -> int {
+    if (int rc = lim()) return rc;
+    hipExtLaunchKernelGGL(kern, dim3(p.grid_b), dim3(kBlock), p.lds_b, st, ev ? ev[2] : nullptr,
+                          ev ? ev[3] : nullptr, 0, p.a, (const uint32_t *)w, bitmaps, ft);
+    ADL_HIP_TRY(hipGetLastError());
+    return ADL_OK;
+  };
+  // pass-B units per pipeline stage (ADL_BLOOM_BK_DEPTH, tuning)
+  if (p.depth_b >= 16) return go_b(adl_host::lds_limit<bk_tile_kernel<16, DT>>, bk_tile_kernel<16, DT>);
+  if (p.depth_b <= 4) return go_b(adl_host::lds_limit<bk_tile_kernel<4, DT>>, bk_tile_kernel<4, DT>);
+  return go_b(adl_host::lds_limit<bk_tile_kernel<8, DT>>, bk_tile_kernel<8, DT>);
 }
 
 std::vector<uint64_t> group_counts(const uint64_t *key_begin, uint32_t nf) {
@@ -629,20 +792,50 @@ uint64_t workspace_bytes(const uint64_t *counts, uint32_t nf, int32_t bpk) {
   return p.ws_bytes;
 }
 
-int build16(const uint4 *d_keys, const uint64_t *key_begin, uint32_t nf, int32_t bpk, uint8_t *d_bitmaps,
-            const uint64_t *bitmap_off, void *ws, uint64_t ws_bytes, hipStream_t st, hipEvent_t *ev) {
+namespace {
+template <class Src>
+int build_src(Src src, const uint64_t *key_begin, uint64_t key0, uint32_t nf, int32_t bpk, uint8_t *d_bitmaps,
+              const uint64_t *bitmap_off, void *ws, uint64_t ws_bytes, hipStream_t st, hipEvent_t *ev) {
   const std::vector<uint64_t> counts = group_counts(key_begin, nf);
   BkPlan p;
   if (int rc = make_plan(counts.data(), nf, bpk, p)) return rc;
   if (!ws || ws_bytes < p.ws_bytes) return ADL_ERR_WORKSPACE;
   for (uint32_t f = 0; f < nf; ++f) {
     if (bitmap_off[f] % 16) return ADL_ERR_INVALID_ARG;
-    p.f[f].key_begin = key_begin[f];
+    p.f[f].key_begin = key_begin[f] - key0;
     p.f[f].bitmap_off = bitmap_off[f];
     if (!p.dt) p.a.f[f] = p.f[f];
   }
-  return p.dt ? launch<true>(p, d_keys, d_bitmaps, ws, st, ev) : launch<false>(p, d_keys, d_bitmaps, ws, st, ev);
+  return p.dt ? launch<true>(p, src, d_bitmaps, ws, st, ev) : launch<false>(p, src, d_bitmaps, ws, st, ev);
 }
+}  // namespace
+
+int build16(const uint4 *d_keys, const uint64_t *key_begin, uint32_t nf, int32_t bpk, uint8_t *d_bitmaps,
+            const uint64_t *bitmap_off, void *ws, uint64_t ws_bytes, hipStream_t st, hipEvent_t *ev) {
+  return build_src(BkSrc16{d_keys}, key_begin, 0, nf, bpk, d_bitmaps, bitmap_off, ws, ws_bytes, st, ev);
+}
+
+int var_layout(const uint64_t *counts, uint32_t nf, int32_t bpk, uint64_t *pair_off, uint64_t *scratch_off) {
+  BkPlan p;
+  if (int rc = make_plan(counts, nf, bpk, p)) return rc;
+  *pair_off = p.pair_off;
+  *scratch_off = p.scratch_off;
+  return ADL_OK;
+}
+
+int build_pairs(const uint2 *d_pairs, const uint64_t *key_begin, uint32_t nf, int32_t bpk, uint8_t *d_bitmaps,
+                const uint64_t *bitmap_off, void *ws, uint64_t ws_bytes, hipStream_t st, hipEvent_t *ev) {
+  return build_src(BkSrcPairs{d_pairs}, key_begin, key_begin[0], nf, bpk, d_bitmaps, bitmap_off, ws, ws_bytes, st,
+                   ev);
+}
+
+#ifdef ADL_BLOOM_STAMPS
+int debug_stamps(uint64_t *out, uint64_t n) {
+  const uint64_t bytes = std::min<uint64_t>(n, 2 * 256 * 16 * 8) * 8;
+  ADL_HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_bk_stamps), bytes, 0, hipMemcpyDeviceToHost));
+  return ADL_OK;
+}
+#endif
 
 int positions(const uint64_t *counts, uint32_t nf, int32_t bpk, const void *ws, uint64_t *out, hipStream_t st) {
   BkPlan p;

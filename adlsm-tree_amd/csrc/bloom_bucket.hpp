@@ -24,9 +24,25 @@ __attribute__((visibility("hidden"))) int build16(const uint4 *d_keys, const uin
                                                   int32_t bpk, uint8_t *d_bitmaps, const uint64_t *bitmap_off,
                                                   void *ws, uint64_t ws_bytes, hipStream_t st, hipEvent_t *ev);
 
+// Variable-length keys: bloom_build.hip's hashing pass writes (h1, h2) of
+// every key of the group at d_pairs[key index - key_begin[0]] (any order
+// inside a filter's range), in the workspace at byte *pair_off; past
+// kMaxFilt filters its descriptor table goes to byte *scratch_off.  Then
+// build_pairs runs the two passes over the pairs.
+__attribute__((visibility("hidden"))) int var_layout(const uint64_t *counts, uint32_t nf, int32_t bpk,
+                                                     uint64_t *pair_off, uint64_t *scratch_off);
+__attribute__((visibility("hidden"))) int build_pairs(const uint2 *d_pairs, const uint64_t *key_begin, uint32_t nf,
+                                                      int32_t bpk, uint8_t *d_bitmaps, const uint64_t *bitmap_off,
+                                                      void *ws, uint64_t ws_bytes, hipStream_t st, hipEvent_t *ev);
+
 // Sum of the entries the last build16 over these filters routed (the count
 // tables in the workspace); instrumentation for the bench line.
 __attribute__((visibility("hidden"))) int positions(const uint64_t *counts, uint32_t nf, int32_t bpk, const void *ws,
                                                     uint64_t *out, hipStream_t st);
+
+#ifdef ADL_BLOOM_STAMPS
+// diagnostics build: the bucketed passes' phase stamps [pass][workgroup][phase]
+__attribute__((visibility("hidden"))) int debug_stamps(uint64_t *out, uint64_t n);
+#endif
 
 }  // namespace adl_bk

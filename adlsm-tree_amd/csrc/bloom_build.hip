@@ -1483,6 +1483,69 @@ int launch_atomic(const Plan &p, Keys keys, uint8_t *d_bitmaps, hipStream_t st) 
   return ADL_OK;
 }
 
+// The var-len hashing pass for the bucketed build (bloom_bucket.hip): (h1, h2)
+// of filter f's keys at pairs[key_begin[f] - key_begin[0] + ...], each run of
+// hv_keys keys in its length-sorted order (the bitmap is an OR, so the order
+// inside a filter's range does not matter).  hash_var_kernel unchanged: a
+// plan with C = 1 whose chunk_base is the filter's pair offset.  Past
+// kMaxFilters filters its descriptors and run map go to `scratch`
+// (adl_bk::var_layout).  ev0: the profiled pass-A interval opens here.
+int hash_pairs_var(KeysVar keys, const uint64_t *key_begin, uint32_t nf, uint2 *pairs, uint8_t *scratch,
+                   hipStream_t st, hipEvent_t ev0) {
+  static_assert(sizeof(FilterDesc) <= 128, "adl_bk::make_plan reserves 128 B per filter for this table");
+  BuildArgs a;
+  memset(&a, 0, sizeof(a));
+  a.nf = nf;
+  a.C = 1;
+  const uint32_t hk = env_u32("ADL_BLOOM_HV_KEYS", 512);
+  a.hv_keys = hk <= 256 ? 256 : hk <= 512 ? 512 : hk <= 1024 ? 1024 : 2048;
+#ifdef ADL_BLOOM_STAMPS
+  a.exp = env_u32("ADL_BLOOM_EXP", 0);
+#endif
+  std::vector<FilterDesc> fd(nf);
+  uint32_t sc = 0;
+  for (uint32_t f = 0; f < nf; ++f) {
+    FilterDesc &d = fd[f];
+    d = FilterDesc{};
+    d.key_begin = key_begin[f];
+    d.n = (uint32_t)(key_begin[f + 1] - key_begin[f]);
+    d.chunk_base = (uint32_t)(key_begin[f] - key_begin[0]);
+    d.sc_base = sc;
+    sc += (d.n + a.hv_keys - 1) / a.hv_keys;
+  }
+  if (!sc) {  // no keys: an empty hashing interval
+    if (ev0) ADL_HIP_TRY(hipEventRecord(ev0, st));
+    return ADL_OK;
+  }
+  const bool dt = nf > (uint32_t)kMaxFilters;
+  FilterTable ft{};
+  if (dt) {
+    FilterDesc *d_fd = reinterpret_cast<FilterDesc *>(scratch);
+    uint32_t *sc_f = reinterpret_cast<uint32_t *>(scratch + adl_host::round_up(nf * sizeof(FilterDesc), 256));
+    if (int rc = adl_host::t_upload.upload(d_fd, fd.data(), nf * sizeof(FilterDesc), st)) return rc;
+    // chunks = tiles = 0: only the run map is filled
+    hipLaunchKernelGGL(fill_maps_kernel, dim3(nf), dim3(256), 0, st, d_fd, sc_f, sc_f, sc_f, a.hv_keys);
+    ADL_HIP_TRY(hipGetLastError());
+    ft.fd = (cptr<FilterDesc>)d_fd;
+    ft.sc_f = (cptr<uint32_t>)sc_f;
+  } else {
+    std::copy(fd.begin(), fd.end(), a.f);
+  }
+  auto go = [&](auto lim, auto kern, size_t lds) -> int {
+    if (int rc = lim()) return rc;
+    hipExtLaunchKernelGGL(kern, dim3(sc), dim3(kHvBlock), lds, st, ev0, nullptr, 0, a, keys, pairs, sc, ft);
+    ADL_HIP_TRY(hipGetLastError());
+    return ADL_OK;
+  };
+#define ADL_HV(S)                                                                                          \
+  (dt ? go(adl_host::lds_limit<hash_var_kernel<S, true>>, hash_var_kernel<S, true>, hv_lds_bytes<S>())   \
+      : go(adl_host::lds_limit<hash_var_kernel<S, false>>, hash_var_kernel<S, false>, hv_lds_bytes<S>()))
+  const int rc = a.hv_keys == 256 ? ADL_HV(256) : a.hv_keys == 512 ? ADL_HV(512) : a.hv_keys == 1024 ? ADL_HV(1024)
+                                                                                                   : ADL_HV(2048);
+#undef ADL_HV
+  return rc;
+}
+
 }  // namespace
 
 namespace {
@@ -1532,6 +1595,33 @@ int build_groups(const uint8_t *d_keys, const uint64_t *d_offsets, uint32_t key_
       const int rc = adl_bk::build16(reinterpret_cast<const uint4 *>(d_keys), key_begin + g, nf, bpk, d_bitmaps,
                                      bitmap_off + g, wsa, wsb, st, prof_slot());
       if (rc) return rc;
+      t_last_bk = true;
+      g = e;
+      continue;
+    }
+    // variable-length keys (16-byte-aligned buffer): the hashing pass into
+    // (h1, h2) pairs, then the bucketed build over the pairs
+    if (!atomic && d_offsets && (reinterpret_cast<uintptr_t>(d_keys) % 16) == 0 &&
+        !(flags & ADL_BLOOM_SKIP_ADJACENT_DUPLICATES) && adl_host::env_on("ADL_BLOOM_BK", true) &&
+        adl_host::env_on("ADL_BLOOM_VAR_HASH", true) && adl_bk::workspace_bytes(counts.data(), nf, bpk)) {
+      uint8_t *wsa = nullptr;
+      uint64_t wsb = 0, pair_off = 0, scratch_off = 0;
+      if (d_workspace) {
+        wsa = reinterpret_cast<uint8_t *>(adl_host::round_up(reinterpret_cast<uintptr_t>(d_workspace), 256));
+        const uint64_t skip = (uint64_t)(wsa - static_cast<uint8_t *>(d_workspace));
+        wsb = workspace_bytes > skip ? workspace_bytes - skip : 0;
+      }
+      if (!wsa || wsb < adl_bk::workspace_bytes(counts.data(), nf, bpk)) return ADL_ERR_WORKSPACE;
+      if (int rc = adl_bk::var_layout(counts.data(), nf, bpk, &pair_off, &scratch_off)) return rc;
+      uint2 *pairs = reinterpret_cast<uint2 *>(wsa + pair_off);
+      hipEvent_t *ev = prof_slot();
+      if (int rc = hash_pairs_var(KeysVar{d_keys, d_offsets}, key_begin + g, nf, pairs, wsa + scratch_off, st,
+                                  ev ? ev[0] : nullptr))
+        return rc;
+      hipEvent_t evb[4] = {nullptr, ev ? ev[1] : nullptr, ev ? ev[2] : nullptr, ev ? ev[3] : nullptr};
+      if (int rc = adl_bk::build_pairs(pairs, key_begin + g, nf, bpk, d_bitmaps, bitmap_off + g, wsa, wsb, st,
+                                       ev ? evb : nullptr))
+        return rc;
       t_last_bk = true;
       g = e;
       continue;
@@ -1596,10 +1686,13 @@ int adl_bloom_test_fault(int site, int64_t arg) {
 
 #ifdef ADL_BLOOM_STAMPS
 // Diagnostics build only: copies g_stamps ([pass][workgroup][phase] cycles).
+// Past those, the bucketed build's [2][2048][8] (bloom_bucket.hip).
 int adl_bloom_debug_stamps(uint64_t *out, uint64_t n) {
-  const uint64_t bytes = std::min<uint64_t>(n, 3 * 2048 * 8) * 8;
+  constexpr uint64_t kOwn = 3 * 2048 * 8;
+  const uint64_t bytes = std::min<uint64_t>(n, kOwn) * 8;
   ADL_HIP_TRY(hipDeviceSynchronize());
   ADL_HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), bytes, 0, hipMemcpyDeviceToHost));
+  if (n > kOwn) return adl_bk::debug_stamps(out + kOwn, n - kOwn);
   return ADL_OK;
 }
 #endif

@@ -45,9 +45,24 @@ def main():
     L = adlbloom.lib()
     L.adl_bloom_debug_stamps.restype = ctypes.c_int
     L.adl_bloom_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
-    buf = np.zeros((3, 2048, 8), dtype=np.uint64)
-    assert L.adl_bloom_debug_stamps(buf.ctypes.data, buf.size) == 0
-    for p in ((0, 1, 2) if varlen else (0, 1)):
+    if os.environ.get("BK", "1") != "0":  # the bucketed build (bloom_bucket.hip), the default
+        raw = np.zeros(3 * 2048 * 8 + 2 * 256 * 16 * 8, dtype=np.uint64)
+        assert L.adl_bloom_debug_stamps(raw.ctypes.data, raw.size) == 0
+        bk = raw[3 * 2048 * 8:].reshape(2, 256, 16, 8)
+        names = [["claims + hash", "claim barrier", "flush", "end barrier", "final flush", "slice set-up", "-", "-"],
+                 ["counts + scan", "gather + or", "overflow", "tile barrier", "write + zero", "-", "-", "-"]]
+        for p in (0, 1):
+            print(f"pass {'AB'[p]} (bucketed): mean over 256 workgroups, cycles per phase, by wave")
+            print("  wave " + "".join(f"{n[:13]:>14s}" for n in names[p] if n != "-"))
+            for wv in range(16):
+                row = bk[p, :, wv, :].astype(np.float64).mean(axis=0)
+                print(f"  {wv:4d} " + "".join(f"{row[i]:14.0f}" for i in range(8) if names[p][i] != "-"))
+        del bm
+        return
+    else:
+        buf = np.zeros((3, 2048, 8), dtype=np.uint64)
+        assert L.adl_bloom_debug_stamps(buf.ctypes.data, buf.size) == 0
+    for p in ((0, 1, 2) if varlen and buf.shape[0] == 3 else (0, 1)):
         rows = buf[p][buf[p].sum(axis=1) > 0]
         tot = rows.sum(axis=1).mean()
         print(f"pass {'ABH'[p]}: {len(rows)} workgroups, mean total {tot:.0f} cycles")
