@@ -184,6 +184,28 @@ __device__ __forceinline__ uint32_t ring_word(uint32_t t, uint32_t slot, uint32_
   return (t << lgS) + (slot ^ ((t & 7u) << 2));
 }
 
+// Entry layout.  P3 = false: one u32 position per entry.  P3 = true: 24-bit
+// entries, 4 to 3 words (a tile offset needs 20 bits), so the round trip
+// through HBM moves 3/4 of the bytes; a 16-entry granule is 48 bytes.
+// Region, extent and unit starts are multiples of 16 entries.
+template <bool P3>
+__device__ __forceinline__ uint32_t ent_words(uint32_t e) {
+  return P3 ? (e >> 2) * 3u : e;
+}
+typedef uint32_t u32x3_t __attribute__((ext_vector_type(3)));
+__device__ __forceinline__ u32x3_t pack3(uint4 v) {
+  const uint32_t a = v.x & kTMask, b = v.y & kTMask, c = v.z & kTMask, e = v.w & kTMask;
+  u32x3_t r;
+  r.x = a | (b << 24);
+  r.y = (b >> 8) | (c << 16);
+  r.z = (c >> 16) | (e << 8);
+  return r;
+}
+__device__ __forceinline__ uint4 unpack3(u32x3_t r) {
+  return make_uint4(r.x & 0xffffffu, (r.x >> 24) | ((r.y & 0xffffu) << 8), (r.y >> 16) | ((r.z & 0xffu) << 16),
+                    r.z >> 8);
+}
+
 // ---------------------------------------------------------------- pass A
 // K > 0: k known at compile time (positions and claims unrolled); K == 0:
 // runtime k (a.k), one position at a time.
@@ -210,7 +232,7 @@ struct BkSrcPairs {
   }
 };
 
-template <int K, class Src, bool DT>
+template <int K, class Src, bool DT, bool P3>
 __global__ __launch_bounds__(kBlock) void bk_bin16_kernel(BkArgs a, Src src,
                                                           uint32_t *__restrict__ ws, BkTable ft) {
   using F = BF<DT>;
@@ -244,7 +266,8 @@ __global__ __launch_bounds__(kBlock) void bk_bin16_kernel(BkArgs a, Src src,
     const uint32_t sl = s - d.slice0;
     const uint32_t first = sl * d.L;
     const uint32_t cnt = first < d.n ? min(d.L, d.n - first) : 0u;
-    const uint32_t T = d.T, cap = d.cap, xo = d.xo, tstride = cap + kLink;
+    const uint32_t T = d.T, cap = d.cap, xo = d.xo;
+    const uint32_t tstride = ent_words<P3>(cap) + kLink, xw = ent_words<P3>(xo) + kLink;
     const FastMod mod = d.mod;
     uint32_t *area = ws + d.area_base + (uint64_t)sl * d.stride;
     for (uint32_t t = tid; t < T; t += kBlock) {
@@ -289,15 +312,16 @@ __global__ __launch_bounds__(kBlock) void bk_bin16_kernel(BkArgs a, Src src,
           const uint32_t e = (fl + i) * kGran;  // entry offset in the (slice, tile) stream
           uint32_t tgt;
           if (e < cap) {
-            tgt = t * tstride + e;
+            tgt = t * tstride + ent_words<P3>(e);
           } else {  // past the region: overflow extents from the slice's pool
             const uint32_t eo = e - cap, o = eo % xo;
             if (o == 0) {
-              const uint32_t ext = T * tstride + atomicAdd(bump, xo + kLink);
-              area[eo == 0 ? t * tstride + cap : cur[t] + xo] = ext;  // link from the region / previous extent
+              const uint32_t ext = T * tstride + atomicAdd(bump, xw);
+              // link from the region / previous extent
+              area[eo == 0 ? t * tstride + ent_words<P3>(cap) : cur[t] + ent_words<P3>(xo)] = ext;
               cur[t] = ext;
             }
-            tgt = cur[t] + o;
+            tgt = cur[t] + ent_words<P3>(o);
           }
           wl[pre + i] = make_uint2(t | (((start + i * kGran) & (S - 1)) << 16), tgt);
         }
@@ -314,7 +338,8 @@ __global__ __launch_bounds__(kBlock) void bk_bin16_kernel(BkArgs a, Src src,
           const uint2 le = wl[e];
           const uint32_t tt = le.x & 0xffffu, ro = le.x >> 16, q = lane & 3u;
           const uint4 v = *reinterpret_cast<const uint4 *>(ring + ring_word(tt, ro + 4u * q, lgS));
-          *reinterpret_cast<uint4 *>(area + le.y + 4u * q) = v;
+          if (P3) *reinterpret_cast<u32x3_t *>(area + le.y + 3u * q) = pack3(v);
+          else *reinterpret_cast<uint4 *>(area + le.y + 4u * q) = v;
         }
       }
     };
@@ -448,7 +473,7 @@ __global__ __launch_bounds__(kBlock) void bk_bin16_kernel(BkArgs a, Src src,
 // 64-entry units; wave w takes units [U*w/16, U*(w+1)/16) -- a contiguous
 // stretch of long runs -- and gathers them D units per stage, two stages in
 // flight (unit descriptors computed per lane, handed out by readlane).
-template <int D, bool DT>
+template <int D, bool DT, bool P3>
 __global__ __launch_bounds__(kBlock) void bk_tile_kernel(BkArgs a, const uint32_t *__restrict__ ws,
                                                          uint8_t *__restrict__ bitmaps, BkTable ft) {
   using F = BF<DT>;
@@ -476,7 +501,9 @@ __global__ __launch_bounds__(kBlock) void bk_tile_kernel(BkArgs a, const uint32_
   uint32_t c_next = blockIdx.x < a.total_tiles ? count_of(blockIdx.x) : 0u;
   for (uint32_t tg = blockIdx.x; tg < a.total_tiles; tg += gridDim.x) {
     const auto &d = F::at(a, ft, F::of_tile(a, ft, tg));
-    const uint32_t t = tg - d.tile0, R = d.R, cap = d.cap, tstride = cap + kLink, stride = d.stride;
+    const uint32_t t = tg - d.tile0, R = d.R, cap = d.cap, stride = d.stride;
+    const uint32_t tstride = ent_words<P3>(cap) + kLink, xw = ent_words<P3>(d.xo) + kLink;
+    constexpr uint32_t EPU = P3 ? 4 * kWave : kWave;  // entries per unit (one load per lane)
     const uint32_t *abase = ws + d.area_base;
     // (a count can never exceed the slice's k*L positions; clamped so that a
     // corrupted workspace gives a wrong bitmap, never a wild read or a long walk)
@@ -485,7 +512,7 @@ __global__ __launch_bounds__(kBlock) void bk_tile_kernel(BkArgs a, const uint32_
     if (c > cap) *ovf = 1;
     const uint32_t cf = min(c, cap);
     uint32_t U;
-    const uint32_t ex = block_excl_scan<kBlock>((cf + kWave - 1) / kWave, scratch, &U);  // (barriers inside)
+    const uint32_t ex = block_excl_scan<kBlock>((cf + EPU - 1) / EPU, scratch, &U);  // (barriers inside)
     if (tid < R) {
       pre[tid] = ex;
       cfast[tid] = cf;
@@ -509,11 +536,11 @@ __global__ __launch_bounds__(kBlock) void bk_tile_kernel(BkArgs a, const uint32_
           else hi = mid;
         }
         const uint32_t q = u - pre[lo];
-        doff = lo * stride + t * tstride + q * kWave;
-        dval = min(cfast[lo] - q * kWave, (uint32_t)kWave);
+        doff = lo * stride + t * tstride + ent_words<P3>(q * EPU);
+        dval = min(cfast[lo] - q * EPU, EPU);
       }
       struct Stage {
-        uint32_t v[D];
+        uint32_t v[D][P3 ? 3 : 1];
         uint32_t val[D];  // valid entries of each slot's unit (wave-uniform)
       };
       // A stage's loads are issued unconditionally (a slot past nb reads
@@ -525,14 +552,35 @@ __global__ __launch_bounds__(kBlock) void bk_tile_kernel(BkArgs a, const uint32_
         for (int u = 0; u < D; ++u) {
           const uint32_t i = min(q0 + (uint32_t)u, (uint32_t)kWave - 1u);
           st.val[u] = q0 + (uint32_t)u < nb ? __builtin_amdgcn_readlane(dval, i) : 0u;
-          st.v[u] = abase[__builtin_amdgcn_readlane(doff, i) + (lane < st.val[u] ? lane : 0u)];
+          if (P3) {
+            const u32x3_t r = *reinterpret_cast<const u32x3_t *>(
+                abase + __builtin_amdgcn_readlane(doff, i) + (4u * lane < st.val[u] ? 3u * lane : 0u));
+            st.v[u][0] = r.x;
+            st.v[u][P3 ? 1 : 0] = r.y;
+            st.v[u][P3 ? 2 : 0] = r.z;
+          } else {
+            st.v[u][0] = abase[__builtin_amdgcn_readlane(doff, i) + (lane < st.val[u] ? lane : 0u)];
+          }
         }
       };
       auto consume = [&](const Stage &st, uint32_t) {
 #pragma unroll
         for (int u = 0; u < D; ++u) {
-          if (lane < st.val[u]) {
-            const uint32_t off = st.v[u] & kTMask;
+          if (P3) {
+            u32x3_t r;
+            r.x = st.v[u][0];
+            r.y = st.v[u][P3 ? 1 : 0];
+            r.z = st.v[u][P3 ? 2 : 0];
+            const uint4 e = unpack3(r);
+            const uint32_t ev[4] = {e.x, e.y, e.z, e.w};
+#pragma unroll
+            for (int v = 0; v < 4; ++v)
+              if (4u * lane + (uint32_t)v < st.val[u]) {
+                const uint32_t off = ev[v] & kTMask;
+                atomicOr(&tile[off >> 5], 1u << (off & 31u));
+              }
+          } else if (lane < st.val[u]) {
+            const uint32_t off = st.v[u][0] & kTMask;
             atomicOr(&tile[off >> 5], 1u << (off & 31u));
           }
         }
@@ -552,19 +600,33 @@ __global__ __launch_bounds__(kBlock) void bk_tile_kernel(BkArgs a, const uint32_
       const uint32_t cs = cfull[s];
       if (cs <= cap) continue;
       const uint32_t sb = s * stride;
-      uint32_t lk = sb + t * tstride + cap;
+      uint32_t lk = sb + t * tstride + ent_words<P3>(cap);
       for (uint32_t e = cap; e < cs; e += d.xo) {
         // an extent lies inside the slice's pool (clamped: see the counts)
-        const uint32_t ext =
-            min(__builtin_amdgcn_readfirstlane(abase[lk]), stride - d.xo - kLink);
+        const uint32_t ext = min(__builtin_amdgcn_readfirstlane(abase[lk]), stride - xw);
         const uint32_t nn = min(d.xo, cs - e);
-        for (uint32_t o = 0; o < nn; o += kWave) {
-          if (o + lane < nn) {
-            const uint32_t off = abase[sb + ext + o + lane] & kTMask;
-            atomicOr(&tile[off >> 5], 1u << (off & 31u));
+        if (P3) {
+          for (uint32_t o = 0; o < nn; o += 4 * kWave) {
+            if (o + 4u * lane < nn) {
+              const uint4 ev = unpack3(*reinterpret_cast<const u32x3_t *>(abase + sb + ext + ent_words<P3>(o) + 3u * lane));
+              const uint32_t e4[4] = {ev.x, ev.y, ev.z, ev.w};
+#pragma unroll
+              for (int v = 0; v < 4; ++v)
+                if (o + 4u * lane + (uint32_t)v < nn) {
+                  const uint32_t off = e4[v] & kTMask;
+                  atomicOr(&tile[off >> 5], 1u << (off & 31u));
+                }
+            }
+          }
+        } else {
+          for (uint32_t o = 0; o < nn; o += kWave) {
+            if (o + lane < nn) {
+              const uint32_t off = abase[sb + ext + o + lane] & kTMask;
+              atomicOr(&tile[off >> 5], 1u << (off & 31u));
+            }
           }
         }
-        lk = sb + ext + d.xo;
+        lk = sb + ext + ent_words<P3>(d.xo);
       }
     }
     BK_STAMP(2);  // overflow chains
@@ -603,6 +665,7 @@ struct BkPlan {
   uint64_t pair_off = 0, scratch_off = 0;  // var-len keys: (h1, h2) pairs, then the hashing pass's table
   uint32_t grid_a = 0, grid_b = 0;
   uint32_t depth_b = 8;
+  bool p3 = false;  // 24-bit entries (ADL_BLOOM_BK_P3)
   size_t lds_a = 0, lds_b = 0;
 };
 
@@ -620,6 +683,8 @@ int make_plan(const uint64_t *counts, uint32_t nf, int32_t bpk, BkPlan &p) {
     total_n += counts[f];
   }
   const uint32_t cus = adl_host::device_cus();
+  p.p3 = k == 6 && adl_host::env_on("ADL_BLOOM_BK_P3", false);  // (the runtime-k pass A writes u32 entries)
+  auto words = [&](uint64_t e) { return p.p3 ? e / 4 * 3 : e; };  // entries (multiple of 16) -> words
   // slice size: one slice per CU for the whole group, at least 1024 keys (one batch)
   const uint64_t Lg = std::max<uint64_t>(1024, (total_n + cus - 1) / cus);
   uint64_t area = 0, cntw = 0;  // words of the slice areas; of the count tables (placed after the areas)
@@ -652,9 +717,9 @@ int make_plan(const uint64_t *counts, uint32_t nf, int32_t bpk, BkPlan &p) {
       // extents of xo <= cap - 16 entries: the slice's overflow needs at most
       // ceil(kl / xo) + 2 of them whatever the key distribution
       xo = std::min<uint64_t>(256, (cap - kGran) & ~(uint64_t)(kGran - 1));
-      pool = ((kl + xo - 1) / xo + 2) * (xo + kLink);
+      pool = ((kl + xo - 1) / xo + 2) * (words(xo) + kLink);
     }
-    const uint64_t stride = T * (cap + kLink) + pool;
+    const uint64_t stride = T * (words(cap) + kLink) + pool;
     if (R * stride + kPad >= (1ull << 32)) return ADL_ERR_TOO_LARGE;  // u32 offsets inside a filter's areas
     d.n = (uint32_t)n;
     d.L = (uint32_t)L;
@@ -756,8 +821,10 @@ int launch(BkPlan &p, Src keys, uint8_t *bitmaps, void *ws, hipStream_t st, hipE
       ADL_HIP_TRY(hipGetLastError());
       return ADL_OK;
     };
-    const int rc = p.a.k == 6 ? go(adl_host::lds_limit<bk_bin16_kernel<6, Src, DT>>, bk_bin16_kernel<6, Src, DT>)
-                              : go(adl_host::lds_limit<bk_bin16_kernel<0, Src, DT>>, bk_bin16_kernel<0, Src, DT>);
+    const int rc =
+        p.a.k != 6 ? go(adl_host::lds_limit<bk_bin16_kernel<0, Src, DT, false>>, bk_bin16_kernel<0, Src, DT, false>)
+        : p.p3     ? go(adl_host::lds_limit<bk_bin16_kernel<6, Src, DT, true>>, bk_bin16_kernel<6, Src, DT, true>)
+                   : go(adl_host::lds_limit<bk_bin16_kernel<6, Src, DT, false>>, bk_bin16_kernel<6, Src, DT, false>);
     if (rc) return rc;
   } else if (ev) {  // no keys: an empty pass-A interval
     if (ev[0]) ADL_HIP_TRY(hipEventRecord(ev[0], st));
@@ -771,9 +838,11 @@ int launch(BkPlan &p, Src keys, uint8_t *bitmaps, void *ws, hipStream_t st, hipE
     return ADL_OK;
   };
   // pass-B units per pipeline stage (ADL_BLOOM_BK_DEPTH, tuning)
-  if (p.depth_b >= 16) return go_b(adl_host::lds_limit<bk_tile_kernel<16, DT>>, bk_tile_kernel<16, DT>);
-  if (p.depth_b <= 4) return go_b(adl_host::lds_limit<bk_tile_kernel<4, DT>>, bk_tile_kernel<4, DT>);
-  return go_b(adl_host::lds_limit<bk_tile_kernel<8, DT>>, bk_tile_kernel<8, DT>);
+  const bool p3 = p.p3;
+  if (p3) return go_b(adl_host::lds_limit<bk_tile_kernel<8, DT, true>>, bk_tile_kernel<8, DT, true>);
+  if (p.depth_b >= 16) return go_b(adl_host::lds_limit<bk_tile_kernel<16, DT, false>>, bk_tile_kernel<16, DT, false>);
+  if (p.depth_b <= 4) return go_b(adl_host::lds_limit<bk_tile_kernel<4, DT, false>>, bk_tile_kernel<4, DT, false>);
+  return go_b(adl_host::lds_limit<bk_tile_kernel<8, DT, false>>, bk_tile_kernel<8, DT, false>);
 }
 
 std::vector<uint64_t> group_counts(const uint64_t *key_begin, uint32_t nf) {

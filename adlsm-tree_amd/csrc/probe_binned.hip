@@ -377,7 +377,7 @@ __global__ __launch_bounds__(kBlk) void pb_scatter_kernel(const uint4 *__restric
                                                           const uint32_t *__restrict__ cnt,
                                                           const uint32_t *__restrict__ start,
                                                           uint16_t *__restrict__ dest, uint2 *__restrict__ hs,
-                                                          uint32_t exp) {
+                                                          uint32_t exp, uint32_t flat) {
 #ifndef ADL_BLOOM_STAMPS
   exp = 0;  // diagnostics build only (wrong answers): 8 no hashing, 16 no run stores, 32 no place stores
 #endif
@@ -385,6 +385,7 @@ __global__ __launch_bounds__(kBlk) void pb_scatter_kernel(const uint4 *__restric
   uint2 *lhs = reinterpret_cast<uint2 *>(lds);  // kQB hashes in the block's filter order
   uint32_t *lcnt = lds + 2 * kQB, *lstart = lcnt + F + 1, *lbase = lstart + F + 1, *lcur = lbase + F + 1;
   uint32_t *ltiles = lcur + F + 1, *scratch = ltiles + F + 1;
+  uint16_t *lf = reinterpret_cast<uint16_t *>(scratch + 32);  // flat: filter of each place (kQB)
   const int tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid / kWave;
   // every query's id and key are requested first (unconditionally: a lane
   // past n loads the last query and discards it), so they land while the
@@ -417,13 +418,25 @@ __global__ __launch_bounds__(kBlk) void pb_scatter_kernel(const uint4 *__restric
           hash16(kq[r], h1, h2);
         }
         lhs[place] = make_uint2(h1, h2);
+        if (flat) lf[place] = (uint16_t)b;
       }
       if (!(exp & 32)) dest[i] = place;
     }
   }
   __syncthreads();
-  // run by run: consecutive lanes write consecutive slots (whole lines)
   if (exp & 16) return;
+  if (flat) {
+    // place by place: thread e writes the hashes at place e to its filter's
+    // run, so every lane of every store carries one (runs of ~32 queries
+    // filled only half a wave per store in the per-run loop below)
+    const uint32_t placed = lbase[F];
+    for (uint32_t e = tid; e < placed; e += kBlk) {
+      const uint32_t f = lf[e];
+      hs[lstart[f] + (e - lbase[f])] = lhs[e];
+    }
+    return;
+  }
+  // run by run: consecutive lanes write consecutive slots (whole lines)
   for (uint32_t f = wave; f < F; f += kBlk / kWave) {
     const uint32_t c = lcnt[f], lb = lbase[f], gs = lstart[f];
     for (uint32_t r = lane; r < c; r += kWave) hs[gs + r] = lhs[lb + r];
@@ -867,6 +880,9 @@ int adl_bloom_probe_batch_device(const uint8_t *d_keys, const uint64_t *d_offset
   const uint32_t cus = adl_host::device_cus();
   const size_t lds_k1 = (size_t)(2 * F + 2) * 4;                       // counters + tile counts
   const size_t lds_k3 = (size_t)(2 * kQB + 5 * (F + 1) + 32) * 4;      // hashes + 5 per-filter arrays + scratch
+  // + a 2-byte filter id per place: K3 then writes its runs place by place
+  // (ADL_PB_FLAT=1; default: run by run)
+  const bool k3_flat = lds_k3 + kQB * 2 <= (size_t)kLdsWords * 4 && adl_host::env_on("ADL_PB_FLAT", false);
   const size_t lds_k6 = (size_t)(kQB / 4 + 3 * (F + 1) + 32) * 4;      // answers + 3 per-filter arrays + scratch
   const size_t lds_p1 = (size_t)(kMaxTiles + 4 + 64 + p.k * p.C) * 4;
   const size_t lds_p2 = (size_t)kTileBytes + 64 + (size_t)((F + 1 + 3) & ~3u) * 4 +
@@ -903,8 +919,8 @@ int adl_bloom_probe_batch_device(const uint8_t *d_keys, const uint64_t *d_offset
 #else
     constexpr uint32_t exp = 0;
 #endif
-    hipLaunchKernelGGL(pb_scatter_kernel, dim3(p.nb), dim3(kBlk), lds_k3, st, reinterpret_cast<const uint4 *>(d_keys),
-                       d_filter_id, n, F, p.nb, desc, cnt, start, dest, hs, exp);
+    hipLaunchKernelGGL(pb_scatter_kernel, dim3(p.nb), dim3(kBlk), lds_k3 + (k3_flat ? kQB * 2 : 0), st, reinterpret_cast<const uint4 *>(d_keys),
+                       d_filter_id, n, F, p.nb, desc, cnt, start, dest, hs, exp, k3_flat ? 1u : 0u);
     ADL_HIP_TRY(hipGetLastError());
     // k = 6: two rounds, bits 0 .. split-1 of every query, then the rest for
     // the queries still answered 1 (ADL_PB_SPLIT = 0: one round of all k)
