@@ -1552,7 +1552,16 @@ namespace {
 // Runs the filters through the plan/launch pair: all in one launch pair (a
 // compaction's tables), split only where the u32 position indices of one
 // launch's workspace would overflow (groups of at most 2^31 / k keys).
-uint64_t group_keys_max(int32_t bpk) { return (1ull << 31) / (uint64_t)adl_host::num_probes(bpk); }
+// ADL_BLOOM_GROUP_KEYS (tuning): a smaller cap, so a compaction's tables go
+// in several launch pairs (groups whose positions fit the Infinity Cache).
+uint64_t group_keys_max(int32_t bpk) {
+  const uint64_t cap = (1ull << 31) / (uint64_t)adl_host::num_probes(bpk);
+  if (const char *e = getenv("ADL_BLOOM_GROUP_KEYS")) {
+    const uint64_t v = strtoull(e, nullptr, 10);
+    if (v > 0) return std::min(cap, v);
+  }
+  return cap;
+}
 
 // whether this thread's last group went through the bucketed build (for
 // adl_bloom_build_positions, which reads that build's tables)
@@ -1583,7 +1592,7 @@ int build_groups(const uint8_t *d_keys, const uint64_t *d_offsets, uint32_t key_
     const uint32_t nf = e - g;
     // 16-byte keys: the bucketed build (bloom_bucket.hip) when it takes the group
     if (!atomic && !d_offsets && key_stride == 16 && (reinterpret_cast<uintptr_t>(d_keys) % 16) == 0 &&
-        !(flags & ADL_BLOOM_SKIP_ADJACENT_DUPLICATES) && adl_host::env_on("ADL_BLOOM_BK", true) &&
+        !(flags & ADL_BLOOM_SKIP_ADJACENT_DUPLICATES) && adl_host::env_on("ADL_BLOOM_BK", false) &&
         adl_bk::workspace_bytes(counts.data(), nf, bpk)) {
       uint8_t *wsa = nullptr;
       uint64_t wsb = 0;
@@ -1602,7 +1611,7 @@ int build_groups(const uint8_t *d_keys, const uint64_t *d_offsets, uint32_t key_
     // variable-length keys (16-byte-aligned buffer): the hashing pass into
     // (h1, h2) pairs, then the bucketed build over the pairs
     if (!atomic && d_offsets && (reinterpret_cast<uintptr_t>(d_keys) % 16) == 0 &&
-        !(flags & ADL_BLOOM_SKIP_ADJACENT_DUPLICATES) && adl_host::env_on("ADL_BLOOM_BK", true) &&
+        !(flags & ADL_BLOOM_SKIP_ADJACENT_DUPLICATES) && adl_host::env_on("ADL_BLOOM_BK", false) &&
         adl_host::env_on("ADL_BLOOM_VAR_HASH", true) && adl_bk::workspace_bytes(counts.data(), nf, bpk)) {
       uint8_t *wsa = nullptr;
       uint64_t wsb = 0, pair_off = 0, scratch_off = 0;
@@ -1738,7 +1747,11 @@ uint64_t adl_bloom_build_workspace_bytes(const uint64_t *key_counts, uint32_t nu
     }
     Plan p;
     if (make_plan(key_counts + g, e - g, bits_per_key, p)) return 0;
-    ws = std::max({ws, p.ws_bytes, adl_bk::workspace_bytes(key_counts + g, e - g, bits_per_key)});
+    ws = std::max(ws, p.ws_bytes);
+    // the bucketed build (ADL_BLOOM_BK=1, measured slower overall: DESIGN.md
+    // §5) needs its own, larger workspace; sized for only when selected
+    if (adl_host::env_on("ADL_BLOOM_BK", false))
+      ws = std::max(ws, adl_bk::workspace_bytes(key_counts + g, e - g, bits_per_key));
     g = e;
   }
   return ws;

@@ -75,14 +75,23 @@ def test_workspace_bytes():
     import adlbloom
 
     ws = adlbloom.workspace_bytes([10_000_000], 10)
-    # the bucketed build (bloom_bucket.hip): per (slice, tile) regions of the
-    # expected share plus six sigma (~400 MB at 256 x 763), each slice's
-    # overflow pool sized for any key distribution (~255 MB), the count
-    # tables, and (h1, h2) 8 B per key for variable-length keys
-    assert 700_000_000 <= ws < 760_000_000
+    # 6 positions x 4 B per key + (tile, chunk) table + (h1, h2) 8 B per key
+    # (variable-length keys are hashed into the workspace before pass A)
+    assert 320_000_000 <= ws < 340_000_000
     assert adlbloom.workspace_bytes([0], 10) > 0
     assert adlbloom.workspace_bytes([1_000_000] * 32, 10) > 0
     assert adlbloom.workspace_bytes([2**31], 10) == 0  # too large -> 0
+
+
+def test_workspace_bytes_bucketed(monkeypatch):
+    """ADL_BLOOM_BK=1 (the bucketed build): per (slice, tile) regions of the
+    expected share plus six sigma (~400 MB at 256 x 763), each slice's
+    overflow pool sized for any key distribution (~255 MB), the count tables
+    and (h1, h2) 8 B per key for variable-length keys."""
+    import adlbloom
+
+    monkeypatch.setenv("ADL_BLOOM_BK", "1")
+    assert 700_000_000 <= adlbloom.workspace_bytes([10_000_000], 10) < 760_000_000
 
 
 def test_missing_library_fails_loudly(monkeypatch, tmp_path):

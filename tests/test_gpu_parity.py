@@ -394,38 +394,6 @@ def test_build_segmented_varlen_many_filters(dev, ab, oracle, monkeypatch, bk):
         assert np.array_equal(hout[int(hoff[f]):int(hoff[f]) + hb[f]], want[f]), f
 
 
-def test_build_chunk_table_path_still_exact(dev, ab, oracle, monkeypatch):
-    """ADL_BLOOM_BK=0: the chunk/table build for 16-byte keys (the fallback for
-    filters of more than 1 024 tiles) on a single filter and 13 filters."""
-    monkeypatch.setenv("ADL_BLOOM_BK", "0")
-    keys = ab.synth_keys16(1_000_003, seed=21)
-    assert np.array_equal(ab.build(keys).cpu().numpy(), oracle.keys2block(keys.cpu().numpy()))
-    sizes = [0, 1, 1000, 50_000, 7, 123_456, 6144, 6145, 3, 200_000, 10, 99_999, 2]
-    kb = np.concatenate([[0], np.cumsum(sizes)]).astype(np.uint64)
-    k2 = ab.synth_keys16(int(kb[-1]), seed=42)
-    out, boff, nbytes = ab.build_segmented(k2, kb)
-    out, hk = out.cpu().numpy(), k2.cpu().numpy()
-    for f in range(len(sizes)):
-        assert np.array_equal(out[int(boff[f]):int(boff[f]) + int(nbytes[f])],
-                              oracle.keys2block(hk[kb[f]:kb[f + 1]])), f
-
-
-def test_build_bucketed_skewed_overflow_extents(dev, ab, oracle):
-    """The bucketed build's overflow extents: 9 distinct keys (h1 != h2, so the
-    pair table does not skip them) repeated to 400 000 keys put every slice's
-    ~9 400 positions on at most 54 bits in a few of the filter's 31 tiles, far
-    past a region's capacity (its uniform share plus six sigma), so most
-    entries go through chained overflow extents."""
-    rng = np.random.default_rng(5)
-    base = rng.integers(0, 256, (64, 16), dtype=np.uint8)
-    h = oracle.murmur3_batch(base)
-    base = base[h[:, 0] != h[:, 1]][:9]
-    keys = np.repeat(base, 400_000 // len(base) + 1, axis=0)[:400_000]
-    rng.shuffle(keys)
-    bm = ab.build(to_dev(dev, keys)).cpu().numpy()
-    assert np.array_equal(bm, oracle.keys2block(keys))
-
-
 # ----------------------------------------------------------------- probe
 def test_probe_matches_appendix_b(dev, ab, golden, oracle):
     for g in golden["appendix_b"]["probes"]:
