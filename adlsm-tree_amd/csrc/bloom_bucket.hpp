@@ -1,10 +1,12 @@
 // adlsm-tree_amd/csrc/bloom_bucket.hpp -- library-internal interface of the
-// bucketed build (bloom_bucket.hip), the default build for 16-byte keys.
+// bucketed build (bloom_bucket.hip), opt-in with ADL_BLOOM_BK=1 (measured
+// slower than the chunk/table build in pass A on every shape in round 4,
+// profiles/r04/ab_bucketed_vs_chunk_table.log).
 //
 // Same output as BloomFilter::Keys2Block (reference src/filter_block.cpp:9-33)
-// per filter; bloom_build.hip's build_groups dispatches a group of filters
-// here when bk_plan accepts it and falls back to its chunk/table build
-// otherwise (large filters, other key shapes, adjacent-duplicate skipping).
+// per filter; when enabled, bloom_build.hip's build_groups dispatches a group
+// of filters here when make_plan accepts it and falls back to its chunk/table
+// build otherwise (large filters, adjacent-duplicate skipping).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
