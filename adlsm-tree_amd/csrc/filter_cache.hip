@@ -47,6 +47,7 @@
 
 #include "bloom_common.hpp"
 #include "filter_block_format.hpp"
+#include "probe_server.hpp"
 
 namespace {
 
@@ -104,6 +105,10 @@ struct adl_bloom_filter_cache {
   std::list<Entry> limbo;    // loading (pinned by their put) and dead (pinned by probes)
   std::unordered_map<std::string, Iter> index;  // live entries only
   std::map<uint64_t, uint64_t> free_;           // offset -> size, coalesced
+  // the resident probe server of this cache's small batches (created on the
+  // first one; srv_tried: do not retry a failed creation)
+  adl_srv::Server *srv = nullptr;
+  bool srv_tried = false;
 
   bool alloc(uint64_t size, uint64_t &at) {
     for (auto it = free_.begin(); it != free_.end(); ++it) {
@@ -188,6 +193,7 @@ int adl_bloom_filter_cache_create(uint64_t capacity_bytes, uint32_t max_tables, 
 // No call on the cache may be running or start once this is called.
 int adl_bloom_filter_cache_destroy(adl_bloom_filter_cache *c) {
   if (!c) return ADL_OK;
+  adl_srv::destroy(c->srv);  // stops its kernel before the arena goes
   (void)hipFree(c->arena);
   delete c;
   return ADL_OK;
@@ -329,6 +335,35 @@ int adl_bloom_filter_cache_probe(adl_bloom_filter_cache *c, const char *const *o
     };
     uint64_t uncached = 0;
     for (uint64_t i = 0; i < n; ++i) uncached += !cached[h_table[i]];
+    // A single-key Get (up to adl_srv::kMaxQ queries): the resident server,
+    // no launch.  Its answers arrive after all its reads of the pinned ranges.
+    {
+      const uint64_t kbytes = h_offsets ? h_offsets[n] - h_offsets[0] : n * (uint64_t)key_stride;
+      adl_srv::Server *srv = nullptr;
+      if (adl_srv::eligible(n, kbytes) && adl_host::env_on("ADL_BLOOM_PROBE_SERVER", true)) {
+        std::lock_guard<std::mutex> g(c->mu);
+        if (!c->srv_tried) {
+          c->srv_tried = true;
+          c->srv = adl_srv::create();
+        }
+        srv = c->srv;
+      }
+      if (srv) {
+        uint64_t rng[2 * adl_srv::kMaxQ];
+        const uint64_t a0 = reinterpret_cast<uint64_t>(c->arena);
+        for (uint64_t i = 0; i < n; ++i) {
+          rng[2 * i] = a0 + be[h_table[i]];
+          rng[2 * i + 1] = a0 + be[num_tables + h_table[i]];
+        }
+        int rc = adl_srv::probe(srv, h_keys, h_offsets, key_stride, n, rng, (uint32_t)adl_host::num_probes(c->bpk),
+                                h_out);
+        if (rc == ADL_OK && adl_host::g_test_faults.take(ADL_TEST_FAULT_CACHE_COMPLETION) >= 0) rc = ADL_ERR_DEVICE;
+        unpin_all();
+        if (rc) return rc;
+        if (h_uncached) *h_uncached = uncached;
+        return ADL_OK;
+      }
+    }
     // 2. without the lock: stage keys, offsets, table ids and the range table
     //    in one H2D, one probe launch, one D2H
     const uint64_t key_bytes = h_offsets ? h_offsets[n] : n * (uint64_t)key_stride;

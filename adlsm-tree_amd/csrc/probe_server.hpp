@@ -1,0 +1,28 @@
+// adlsm-tree_amd/csrc/probe_server.hpp -- library-internal interface of the
+// resident single-key probe server (probe_server.hip), used by the filter
+// cache's small batches (filter_cache.hip).
+#pragma once
+#include <stdint.h>
+
+namespace adl_srv {
+
+constexpr uint32_t kMaxQ = 8;           // queries per request
+constexpr uint32_t kMaxKeyBytes = 320;  // key bytes per request
+
+struct Server;
+
+// A server for the calling thread's current device (no kernel runs until the
+// first probe), or nullptr.
+__attribute__((visibility("hidden"))) Server *create();
+// Stops the kernel (if running), waits for it and frees everything.  No probe
+// may be running or start.
+__attribute__((visibility("hidden"))) void destroy(Server *s);
+__attribute__((visibility("hidden"))) bool eligible(uint64_t n, uint64_t key_bytes);
+// n queries (keys by offsets or fixed stride), query q against the device
+// byte range [range[2q], range[2q+1]) of k-probe filter bits; answers to
+// h_out.  Returns ADL_* status.
+__attribute__((visibility("hidden"))) int probe(Server *s, const uint8_t *h_keys, const uint64_t *h_offsets,
+                                                uint32_t key_stride, uint64_t n, const uint64_t *range, uint32_t k,
+                                                uint8_t *h_out);
+
+}  // namespace adl_srv

@@ -267,3 +267,137 @@ def test_pipeline_fault_mid_pipeline(dev, ab, oracle, monkeypatch, pinned):
     for f in (0, 9, 23):
         want = oracle.keys2block(hk[int(kb[f]):int(kb[f + 1])])
         assert np.array_equal(full[int(boff[f]):int(boff[f]) + nbytes[f]], want), f
+
+
+# ------------------------------------------------ resident probe server (single-key Get)
+def _varlen_block(oracle, seed, n, bpk):
+    """A one-filter block over n keys of 0..64 bytes; (key list, block, bitmap)."""
+    rng = np.random.default_rng(seed)
+    keys = [rng.integers(0, 256, int(rng.integers(0, 65)), dtype=np.uint8).tobytes() for _ in range(n)]
+    offs = np.concatenate([[0], np.cumsum([len(k) for k in keys])]).astype(np.uint64)
+    data = np.frombuffer(b"".join(keys) + b"\0", np.uint8)
+    bm = oracle.keys2block(data, offs, bits_per_key=bpk)
+    return keys, oracle.filter_block_final([bm.tobytes()], bpk), bm
+
+
+def _pack(keys):
+    offs = np.concatenate([[0], np.cumsum([len(k) for k in keys])]).astype(np.uint64)
+    return np.frombuffer(b"".join(keys) + b"\0", np.uint8), offs
+
+
+@pytest.mark.parametrize("bpk", [3, 10, 44])
+def test_probe_server_single_keys_vs_oracle(dev, ab, oracle, monkeypatch, bpk):
+    """Batches of 1..8 queries (keys of 0..320 bytes, several tables, an
+    uncached table, a filter index the block does not have) through the
+    resident server equal the oracle and the launched probe."""
+    T = 3
+    tabs = [_varlen_block(oracle, 40 + t + bpk, 3000, bpk) for t in range(T)]
+    cache = ab.FilterCache(16 << 20, max_tables=8, bits_per_key=bpk)
+    oids = [b"srv-%d" % t for t in range(T)] + [b"not-cached"]
+    for o, (_, blk, _) in zip(oids, tabs):
+        cache.put(o, blk)
+    rng = np.random.default_rng(bpk)
+    checked = 0
+    for it in range(400):
+        n = 1 + it % 8
+        table = rng.integers(0, T + 1, n).astype(np.uint32)
+        qs = []
+        for i in range(n):
+            t = int(table[i])
+            if t < T and rng.integers(0, 2):
+                qs.append(tabs[t][0][int(rng.integers(0, 3000))])  # a member
+            else:
+                qs.append(rng.integers(0, 256, int(rng.integers(0, 321 // n)), dtype=np.uint8).tobytes())
+        data, offs = _pack(qs)
+        want = np.array([1 if t == T else
+                         int(oracle.probe(data, tabs[t][2], offsets=offs[i:i + 2].copy(), bits_per_key=bpk)[0])
+                         for i, t in enumerate(table)], np.uint8)
+        got, unc = cache.probe(oids, table, data, offs)
+        assert np.array_equal(got, want), (it, got, want)
+        assert unc == int((table == T).sum())
+        monkeypatch.setenv("ADL_BLOOM_PROBE_SERVER", "0")
+        got2, _ = cache.probe(oids, table, data, offs)
+        monkeypatch.delenv("ADL_BLOOM_PROBE_SERVER")
+        assert np.array_equal(got2, want)
+        # filter 1 does not exist in these one-filter blocks: absent
+        got3, _ = cache.probe(oids, table, data, offs, filter=1)
+        assert np.array_equal(got3, (table == T).astype(np.uint8))
+        checked += n
+    assert checked > 1500
+    cache.close()
+
+
+def test_probe_server_relaunch_and_teardown(dev, ab, oracle, monkeypatch):
+    """A server that exits when idle (100 us) or at its life limit (2 ms) is
+    relaunched by the next request; closing the cache while the server is
+    running stops it; an armed completion fault fails one call only."""
+    monkeypatch.setenv("ADL_BLOOM_SERVER_IDLE_US", "100")
+    monkeypatch.setenv("ADL_BLOOM_SERVER_LIFE_US", "2000")
+    keys, blk = _block(oracle, 3100, 20_000)
+    bm = oracle.keys2block(keys)
+    q = np.concatenate([keys[:300], oracle.splitmix_keys16(0xD00D, 300)])
+    want = oracle.probe(q, bm)
+    for round_ in range(3):
+        cache = ab.FilterCache(8 << 20, max_tables=8)
+        cache.put(b"t0", blk)
+        t = np.zeros(1, np.uint32)
+        for i in range(len(q)):
+            got, _ = cache.probe([b"t0"], t, q[i:i + 1])
+            assert got[0] == want[i], (round_, i)
+            if i % 97 == 0:
+                time.sleep(0.002)  # idle: the server exits, the next call relaunches it
+        ab.test_fault(ab.TEST_FAULT_CACHE_COMPLETION, 0)
+        try:
+            with pytest.raises(ab.AdlBloomError):
+                cache.probe([b"t0"], t, q[:1])
+        finally:
+            ab.test_fault(ab.TEST_FAULT_CACHE_COMPLETION, -1)
+        got, _ = cache.probe([b"t0"], t, q[:1])
+        assert got[0] == want[0]
+        cache.close()  # the server is (most likely) still running here
+
+
+def test_probe_server_threads(dev, ab, oracle):
+    """8 threads issuing single-key probes at once (one server slot each),
+    while a ninth runs large batches on its own stream: every answer exact,
+    and the large batches are not held up behind the resident kernel."""
+    T = 4
+    tabs = [_block(oracle, 3200 + t, 20_000) for t in range(T)]
+    cache = ab.FilterCache(32 << 20, max_tables=8)
+    oids = [b"th-%d" % t for t in range(T)]
+    for o, (_, blk) in zip(oids, tabs):
+        cache.put(o, blk)
+    rng = np.random.default_rng(9)
+    n = 2000
+    table = rng.integers(0, T, n).astype(np.uint32)
+    fresh = oracle.splitmix_keys16(0xABCD, n)
+    q = np.where((rng.integers(0, 2, n) == 1)[:, None],
+                 np.stack([tabs[t][0][(3 * i) % 20_000] for i, t in enumerate(table)]), fresh)
+    want = np.empty(n, np.uint8)
+    for t in range(T):
+        sel = table == t
+        want[sel] = oracle.probe(q[sel], oracle.keys2block(tabs[t][0]))
+    errors, big_ms = [], []
+
+    def single(k):
+        for i in range(k, n, 8):
+            got, _ = cache.probe(oids, table[i:i + 1], q[i:i + 1])
+            if got[0] != want[i]:
+                errors.append((k, i))
+
+    def big():
+        for _ in range(10):
+            t0 = time.perf_counter()
+            got, _ = cache.probe(oids, table, q)
+            big_ms.append((time.perf_counter() - t0) * 1e3)
+            if not np.array_equal(got, want):
+                errors.append(("big", int((got != want).sum())))
+
+    th = [threading.Thread(target=single, args=(k,)) for k in range(8)] + [threading.Thread(target=big)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    cache.close()
+    assert not errors, errors[:5]
+    assert sorted(big_ms)[len(big_ms) // 2] < 15.0, big_ms
