@@ -36,6 +36,8 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
+#include <random>
 #include <mutex>
 #include <type_traits>
 #include <vector>
@@ -58,6 +60,7 @@ constexpr uint32_t kHistMax = 2049; // tiles per filter + 1 (m < 2^31, TL >= ...
 constexpr uint32_t kMinTileLog2 = 10;
 constexpr uint32_t kMaxTileLog2 = 20;     // 128 KiB LDS tile
 constexpr uint32_t kTargetWorkgroups = 512;
+constexpr uint32_t kHotN = 4096;          // collapsed-key indices per filter (hash16h)
 
 struct FilterDesc {
   uint64_t key_begin;   // first key (index into the key set)
@@ -96,6 +99,19 @@ struct BuildArgs {
   uint32_t var_hash;   // variable-length keys: length-sorted hashing pass + pass A over (h1, h2) (ADL_BLOOM_VAR_HASH)
   uint32_t exp;        // diagnostics build only (ADL_BLOOM_EXP bits, wrong results): pass A 1 no hash,
                        // 2 no position stores, 32 no reduction; pass B 4 no ds_or, 8 no bitmap stores
+  // Collapsed 16-byte keys (hash16h, ADL_BLOOM_HOT): pass A stamps each present
+  // index i of a filter (stamps[f*kHotN + i] = nonce, a value unique to this
+  // launch pair) instead of binning the key's k positions; pass B ORs
+  // (j+1)*hot_h16(i) % m for the stamped indices into its tiles.  Set by the
+  // host per launch: pass A's flag only for bloom_bin16_kernel over 16-byte keys.
+  uint32_t hot;
+  // Live-key compaction (with hot; ADL_BLOOM_COMPACT): the keys of a chunk that
+  // still bin positions (valid, not collapsed) are ranked across the workgroup
+  // and their (h1, h2) staged densely in LDS, so the count and scatter run over
+  // ceil(live / BLOCK) key slots.
+  uint32_t compact;
+  uint64_t nonce;
+  uint64_t *stamps;
   FilterDesc f[kMaxFilters];
 };
 
@@ -689,6 +705,10 @@ struct Src16 {
     return load_nt(keys + d.key_begin + first + idx);
   }
   __device__ static __forceinline__ void hash(const Raw &r, uint32_t &h1, uint32_t &h2) { hash16(r, h1, h2); }
+  // hot: collapsed key, h1 = its index (hash16h)
+  __device__ static __forceinline__ void hash_hot(const Raw &r, uint32_t &h1, uint32_t &h2, bool &hot, bool en) {
+    hash16h(r, h1, h2, hot, en);
+  }
 };
 
 typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
@@ -704,6 +724,10 @@ struct SrcH {
     h1 = r.x;
     h2 = r.y;
   }
+  __device__ static __forceinline__ void hash_hot(const Raw &r, uint32_t &h1, uint32_t &h2, bool &hot, bool) {
+    hash(r, h1, h2);
+    hot = false;
+  }
 };
 
 // Pass A for the hot path (16-byte keys, compile-time k).  Same output as
@@ -715,7 +739,7 @@ struct SrcH {
 //   prefetch keys of c+2
 // so the murmur work hides under the scatter's LDS latency and the position
 // stores drain under the next count.
-template <int BLOCK, int K, class Src, bool DT>
+template <int BLOCK, int K, class Src, bool DT, bool CMP = false>
 __global__ __launch_bounds__(BLOCK) void bloom_bin16_kernel(BuildArgs a, Src keys,
                                                               uint32_t *__restrict__ pos_ws,
                                                               uint32_t *__restrict__ table_ws,
@@ -768,9 +792,15 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin16_kernel(BuildArgs a, Src key
   Raw raw[KPT];
   uint32_t h1[KPT], h2[KPT];
   if (slot >= total_chunks) return;
+  const bool hot_on = a.hot != 0;
+  uint32_t hotm = 0;  // bit i: key slot i collapsed (h1[i] holds its index; hash16h)
   fetch(slot, raw);
 #pragma unroll
-  for (int i = 0; i < KPT; ++i) Src::hash(raw[i], h1[i], h2[i]);
+  for (int i = 0; i < KPT; ++i) {
+    bool ht;
+    Src::hash_hot(raw[i], h1[i], h2[i], ht, hot_on);
+    hotm |= (uint32_t)ht << i;
+  }
   fetch(min(slot + G, total_chunks - 1), raw);
   for (uint32_t i = tid; i < a.hist_words; i += BLOCK) hist[i] = 0;
 
@@ -785,11 +815,66 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin16_kernel(BuildArgs a, Src key
   // 90 % of the repeats) claim, a 32-bit CAS of h1 into a table of twice the
   // slots.
   const uint32_t dd = a.dd_log2, dd2 = a.dd_mode == 2;
-  unsigned long long *dtab = reinterpret_cast<unsigned long long *>(lpos + K * C);
-  uint32_t *dtab32 = lpos + K * C;
+  // With collapsed keys on, the first 2 * kHotN/32 words of that area are this
+  // workgroup's masks of the indices it met in its current and next filter
+  // (hpar selects the current one), and the pair table follows.
+  uint32_t *hmask = lpos + K * C;
+  unsigned long long *dtab = reinterpret_cast<unsigned long long *>(lpos + K * C + (hot_on ? 2 * kHotN / 32 : 0));
+  uint32_t *dtab32 = reinterpret_cast<uint32_t *>(dtab);
   constexpr unsigned long long kEmpty = ~0ull;
   if (dd)
     for (uint32_t i = tid; i < (1u << dd); i += BLOCK) dtab[i] = kEmpty;
+  if (hot_on)
+    for (uint32_t i = tid; i < 2 * kHotN / 32; i += BLOCK) hmask[i] = 0;
+
+  // Compaction, phase 1 (chunk nwg hashed in h1/h2, hotm its collapsed slots):
+  // mark the collapsed keys in hmask[par], rank this thread's live keys in its
+  // wave and publish the wave's total in scratch[wave].  Phase 2, after a
+  // barrier: stage the live pairs densely at the start of lpos (which then
+  // holds no positions: each chunk's positions are stored out before its
+  // successor's keys are staged); returns the chunk's live keys.
+  const int lane = tid & (kWave - 1);
+  uint2 *lst = reinterpret_cast<uint2 *>(lpos);
+  auto rank_live = [&](uint32_t nwg, uint32_t par, uint32_t &off) -> uint32_t {
+    const auto &dn = FT::at(a, ft, FT::of_chunk(a, ft, nwg));
+    const uint32_t ncnt = min(C, dn.n - (nwg - dn.chunk_base) * C);
+    uint32_t v = 0;
+#pragma unroll
+    for (int i = 0; i < KPT; ++i)
+      if (tid + i * BLOCK < ncnt) v |= 1u << i;
+    uint32_t *hm = hmask + par * (kHotN / 32);
+#pragma unroll
+    for (int i = 0; i < KPT; ++i)
+      if ((v & hotm) >> i & 1u) atomicOr(&hm[h1[i] >> 5], 1u << (h1[i] & 31));
+    v &= ~hotm;
+    const uint32_t c = __builtin_popcount(v);
+    const uint32_t incl = wave_incl_scan(c, lane);
+    if (lane == kWave - 1) scratch[wave] = incl;
+    off = incl - c;
+    return v;
+  };
+  auto stage_live = [&](uint32_t v, uint32_t off) -> uint32_t {
+    uint32_t L = 0;
+#pragma unroll
+    for (int q = 0; q < BLOCK / kWave; ++q) {
+      const uint32_t t = scratch[q];
+      off += q < wave ? t : 0u;
+      L += t;
+    }
+#pragma unroll
+    for (int i = 0; i < KPT; ++i) {
+      if ((v >> i) & 1u) lst[off++] = make_uint2(h1[i], h2[i]);
+    }
+    return L;
+  };
+  uint32_t hpar = 0, nlive = 0;
+  if constexpr (CMP) {
+    __syncthreads();  // hmask cleared
+    uint32_t off;
+    const uint32_t v = rank_live(slot, 0, off);
+    __syncthreads();  // wave totals published
+    nlive = stage_live(v, off);
+  }
 
   uint4 *pdst = dummy4;  // deferred store of the previous chunk
   uint32_t ptotal = 0;
@@ -801,15 +886,34 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin16_kernel(BuildArgs a, Src key
     const uint32_t cnt = min(C, d.n - w * C);
     const uint32_t T = d.tiles;
     const FastMod mod = d.mod;
-    __syncthreads();  // hist cleared; the previous scatter is complete in lpos
+    __syncthreads();  // hist cleared; the previous scatter is complete in lpos; the live keys staged
     STAMP(0);
 
     // count(c) + store(c-1)
     const uint32_t pvec = ptotal >> 2;
     uint32_t live = 0;  // bit i: key slot i is counted
+    if constexpr (CMP) {  // dense slots: the staged live keys
 #pragma unroll
-    for (int i = 0; i < KPT; ++i)
-      if (tid + i * BLOCK < cnt) live |= 1u << i;
+      for (int i = 0; i < KPT; ++i) {
+        const uint32_t s = tid + i * BLOCK;
+        if (s < nlive) {
+          const uint2 v = lst[s];
+          h1[i] = v.x;
+          h2[i] = v.y;
+          live |= 1u << i;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < KPT; ++i)
+        if (tid + i * BLOCK < cnt) live |= 1u << i;
+      if (hot_on) {  // a collapsed key marks its index and bins nothing
+#pragma unroll
+        for (int i = 0; i < KPT; ++i)
+          if ((live & hotm) >> i & 1u) atomicOr(&hmask[h1[i] >> 5], 1u << (h1[i] & 31));
+        live &= ~hotm;
+      }
+    }
     if (dd && dd2) {
       uint32_t old[KPT];
 #pragma unroll
@@ -848,17 +952,19 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin16_kernel(BuildArgs a, Src key
 #pragma unroll
         for (int j = 0; j < K; ++j) atomicAdd(&hist[pos[i][j] >> TL], 1u);
       }
+      if constexpr (!CMP) {
 #pragma unroll
-      for (int sv = i * SPI; sv < (i + 1) * SPI && sv < VPT; ++sv) {
-        const uint32_t v = tid + sv * BLOCK;
-        bool ok = v < pvec;
+        for (int sv = i * SPI; sv < (i + 1) * SPI && sv < VPT; ++sv) {
+          const uint32_t v = tid + sv * BLOCK;
+          bool ok = v < pvec;
 #ifdef ADL_BLOOM_STAMPS
-        if (a.exp & 2) ok = false;
+          if (a.exp & 2) ok = false;
 #endif
-        *(ok ? pdst + v : dummy4) = src4[ok ? v : 0u];
+          *(ok ? pdst + v : dummy4) = src4[ok ? v : 0u];
+        }
       }
     }
-    {
+    if constexpr (!CMP) {
       const bool ok = (uint32_t)tid < (ptotal & 3u);
       *(ok ? reinterpret_cast<uint32_t *>(pdst) + pvec * 4 + tid : dummy) = lpos[ok ? pvec * 4 + tid : 0u];
     }
@@ -880,6 +986,7 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin16_kernel(BuildArgs a, Src key
 
     // scatter(c) + hash(c+1) (its keys arrived during the previous chunk;
     // lanes past the end hash a clamped key and never use the result)
+    uint32_t hotn = 0;
 #pragma unroll
     for (int i = 0; i < KPT; ++i) {
       if ((live >> i) & 1u) {
@@ -895,17 +1002,55 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin16_kernel(BuildArgs a, Src key
         h2[i] = raw[i].y | 1u;
       } else
 #endif
-      Src::hash(raw[i], h1[i], h2[i]);
+      {
+        bool ht;
+        Src::hash_hot(raw[i], h1[i], h2[i], ht, hot_on);
+        hotn |= (uint32_t)ht << i;
+      }
     }
+    hotm = hotn;
     fetch(min(wg + 2 * G, total_chunks - 1), raw);
-    __syncthreads();  // lpos holds chunk c sorted; hist is free
+    // the pair table and the index mask hold one filter's keys (positions depend on m)
+    const bool last_of_filter = wg + G >= total_chunks || FT::of_chunk(a, ft, wg + G) != fcur;
+    uint32_t nv = 0, noff = 0;
+    if (CMP && wg + G < total_chunks) nv = rank_live(wg + G, hpar ^ (uint32_t)last_of_filter, noff);
+    __syncthreads();  // lpos holds chunk c sorted; hist is free; this chunk's marks are in hmask
     STAMP(4);
     for (uint32_t i = tid; i <= T; i += BLOCK) hist[i] = 0;
-    // the pair table holds one filter's pairs (positions depend on m)
-    if (dd && wg + G < total_chunks && FT::of_chunk(a, ft, wg + G) != fcur)
+    if (dd && last_of_filter && wg + G < total_chunks)
       for (uint32_t i = tid; i < (1u << dd); i += BLOCK) dtab[i] = kEmpty;
-    pdst = reinterpret_cast<uint4 *>(pos_ws + d.pos_base + (uint64_t)w * a.cap);
-    ptotal = total;
+    if (hot_on && last_of_filter && tid < (int)(kHotN / 32)) {
+      // stamp the indices this workgroup met in filter fcur (every store
+      // issued, unmarked ones to the wave's scratch line) and clear the mask
+      uint32_t *hm = hmask + (CMP ? hpar : 0u) * (kHotN / 32);
+      const uint32_t mw = hm[tid];
+      hm[tid] = 0;
+      unsigned long long *st = reinterpret_cast<unsigned long long *>(a.stamps) + (uint64_t)fcur * kHotN + tid * 32u;
+#pragma unroll 8
+      for (int b = 0; b < 32; ++b)
+        *(((mw >> b) & 1u) ? st + b : reinterpret_cast<unsigned long long *>(dummy)) = a.nonce;
+    }
+    if constexpr (CMP) {
+      hpar ^= (uint32_t)last_of_filter;
+      // this chunk's positions out of lpos now, then the next chunk's live keys in
+      uint4 *dst = reinterpret_cast<uint4 *>(pos_ws + d.pos_base + (uint64_t)w * a.cap);
+      const uint32_t tv = total >> 2;
+#pragma unroll
+      for (int sv = 0; sv < VPT; ++sv) {
+        const uint32_t v = tid + sv * BLOCK;
+        const bool ok = v < tv;
+        *(ok ? dst + v : dummy4) = src4[ok ? v : 0u];
+      }
+      {
+        const bool ok = (uint32_t)tid < (total & 3u);
+        *(ok ? reinterpret_cast<uint32_t *>(dst) + tv * 4 + tid : dummy) = lpos[ok ? tv * 4 + tid : 0u];
+      }
+      __syncthreads();  // lpos read out
+      if (wg + G < total_chunks) nlive = stage_live(nv, noff);
+    } else {
+      pdst = reinterpret_cast<uint4 *>(pos_ws + d.pos_base + (uint64_t)w * a.cap);
+      ptotal = total;
+    }
   }
   // epilogue: the last chunk's store
   const uint32_t pvec = ptotal >> 2;
@@ -998,8 +1143,15 @@ __global__ __launch_bounds__(kBlockB) void bloom_tile_kernel(BuildArgs a,
   }
   STAMP_DECL
 
+  // Collapsed keys (a.hot): thread t holds the positions (j+1)*hot_h16(i) % m
+  // of indices i = t + q*kBlockB, computed once per divisor m.
+  constexpr int kHQ = (int)(kHotN / kBlockB), kHotK = 6;  // pass A's collapsed-key path has k == 6
+  uint32_t hpos[kHQ][kHotK];
+  uint32_t hot_m = 0;  // m that hpos holds positions for (0: none yet)
+
   while (wg < total_tiles) {
-    const auto &d = FT::at(a, ft, FT::of_tile(a, ft, wg));
+    const int fi = FT::of_tile(a, ft, wg);
+    const auto &d = FT::at(a, ft, fi);
     const uint32_t lt = wg - d.tile_base;
     const uint32_t W = d.chunks;
     const uint32_t pos_base = (uint32_t)d.pos_base;
@@ -1007,6 +1159,24 @@ __global__ __launch_bounds__(kBlockB) void bloom_tile_kernel(BuildArgs a,
     if (a.dyn_tiles && tid == 0) qs[1] = atomicAdd(tile_queue, 1u);
     __syncthreads();  // next tile index published
     STAMP(0);
+    if (a.hot) {  // the bits of the collapsed keys pass A stamped for this filter
+      if (d.mod.m != hot_m) {
+        hot_m = d.mod.m;
+#pragma unroll
+        for (int q = 0; q < kHQ; ++q) {
+          const uint32_t F = hot_h16(tid + q * kBlockB);
+          uint32_t x = F;
+#pragma unroll
+          for (int j = 0; j < kHotK; ++j, x += F) hpos[q][j] = fastmod(x, d.mod);
+        }
+      }
+      const unsigned long long *st = reinterpret_cast<const unsigned long long *>(a.stamps) + (uint64_t)fi * kHotN;
+#pragma unroll
+      for (int q = 0; q < kHQ; ++q)
+#pragma unroll
+        for (int j = 0; j < kHotK; ++j)
+          if ((hpos[q][j] >> TL) == lt && st[tid + q * kBlockB] == a.nonce) or_pos(hpos[q][j] & ((1u << TL) - 1u));
+    }
     const uint32_t next = a.dyn_tiles ? qs[1] : wg + G;
     // an empty filter (no chunks) has no batch to prefetch the next tile from
     if (W == 0 && next < total_tiles) fetch_rows(next, 0, pre_s, pre_e);
@@ -1161,6 +1331,9 @@ struct Plan {
   std::vector<FilterDesc> f;  // every filter's descriptor (a.f holds them too when nf <= kMaxFilters)
   bool dt = false;            // more than kMaxFilters: descriptors in the workspace's FilterTable
   uint64_t pos_words = 0, table_words = 0, scratch_words = 0, hash_words = 0, ft_bytes = 0, ws_bytes = 0;
+  uint64_t stamp_off = 0;  // byte offset of the collapsed-key stamps (kHotN u64 per filter)
+  bool hot = false;        // collapsed keys stamped, not binned (16-byte keys, k = 6; ADL_BLOOM_HOT)
+  bool compact = false;    // with hot: pass A compacts the live keys (ADL_BLOOM_COMPACT)
   uint32_t total_chunks = 0, total_tiles = 0, total_sc = 0;
   uint32_t grid_a = 0, grid_b = 0;  // persistent grids
   uint32_t block_a = 512;             // pass A threads per workgroup
@@ -1258,12 +1431,17 @@ int make_plan(const uint64_t *counts, uint32_t nf, int32_t bpk, Plan &p) {
   {
     // pair table in the C + 256 words pass A reserves past the positions
     // (the var-len length sort's area; bloom_bin16_kernel does not use it)
+    // (after the collapsed-key masks' 2 * kHotN / 32 words)
     const uint32_t lg_max = std::min<uint32_t>(env_u32("ADL_BLOOM_DD_LOG2", 11), 12);
     uint32_t lg = 0;
-    while (lg < lg_max && (2u << (lg + 1)) <= C + 256) ++lg;
+    while (lg < lg_max && (2u << (lg + 1)) <= C + 256 - 2 * kHotN / 32) ++lg;
     p.a.dd_log2 = (env_flag("ADL_BLOOM_HASH_DEDUP", 1) && lg >= 4) ? lg : 0;
     p.a.dd_mode = env_u32("ADL_BLOOM_DD_MODE", 2) == 1 ? 1 : 2;
   }
+  // collapsed-key stamping and live-key compaction: bit-exact, measured slower
+  // than binning every key, so opt-in
+  p.hot = env_flag("ADL_BLOOM_HOT", 0) != 0;
+  p.compact = p.hot && env_flag("ADL_BLOOM_COMPACT", 0) != 0;
   {
     const uint32_t hk = env_u32("ADL_BLOOM_HV_KEYS", 512);
     p.a.hv_keys = hk <= 256 ? 256 : hk <= 512 ? 512 : hk <= 1024 ? 1024 : 2048;
@@ -1320,7 +1498,8 @@ int make_plan(const uint64_t *counts, uint32_t nf, int32_t bpk, Plan &p) {
   p.hash_words = adl_host::round_up(2ull * chunk * C, 64);
   // then (more than kMaxFilters) the FilterTable: descriptors, chunk / tile / run maps
   p.ft_bytes = p.dt ? adl_host::round_up(nf * sizeof(FilterDesc), 256) + 4ull * (chunk + tile + sc) + 256 : 0;
-  p.ws_bytes = (p.pos_words + p.table_words + p.scratch_words + p.hash_words) * 4 + p.ft_bytes + 256;
+  p.stamp_off = adl_host::round_up((p.pos_words + p.table_words + p.scratch_words + p.hash_words) * 4 + p.ft_bytes, 256);
+  p.ws_bytes = p.stamp_off + (uint64_t)nf * kHotN * 8 + 256;
   p.lds_a = (size_t)(hist_words + 32 + (k + 1) * C + 256) * 4;
   p.lds_b = (size_t)((1u << (TL - 5)) + 2 * kSegBatch + 4) * 4;
   p.grid_a = std::min<uint32_t>(p.total_chunks, grid_a_max);
@@ -1357,8 +1536,31 @@ inline hipEvent_t *prof_slot() {
   return &t_prof.ev[4 * t_prof.used++];
 }
 
+// A value unique to each launch pair of this process (and, by its random
+// start, to this process): pass A stamps collapsed-key indices with it, and
+// pass B accepts exactly the stamps equal to it, so the stamp area needs no
+// clearing and stamps of earlier builds in the same workspace never count.
+uint64_t next_nonce() {
+  static std::atomic<uint64_t> ctr{[] {
+    std::random_device rd;
+    uint64_t v = ((uint64_t)rd() << 32) ^ rd() ^
+                 (uint64_t)std::chrono::steady_clock::now().time_since_epoch().count() * 0x9e3779b97f4a7c15ull;
+    return v | 1u;
+  }()};
+  uint64_t v;
+  do v = ctr.fetch_add(0x9e3779b97f4a7c15ull * 2, std::memory_order_relaxed);
+  while (v == 0 || v == ~0ull);
+  return v;
+}
+
 template <bool DT, class Keys>
 int launch_binned_dt(const Plan &p, Keys keys, uint8_t *d_bitmaps, void *ws, hipStream_t st) {
+  BuildArgs aa = p.a;
+  aa.stamps = reinterpret_cast<uint64_t *>(reinterpret_cast<uint8_t *>(ws) + p.stamp_off);
+  aa.nonce = next_nonce();
+  aa.hot = 0;
+  aa.compact = 0;
+  uint32_t hot_used = 0;  // pass A stamped collapsed keys: pass B adds their bits
   uint32_t *pos_ws = reinterpret_cast<uint32_t *>(ws);
   uint32_t *tab_ws = pos_ws + p.pos_words;
   uint32_t *queue = tab_ws + p.table_words;  // pass B tile queue, then pass A's scratch lines
@@ -1398,9 +1600,17 @@ int launch_binned_dt(const Plan &p, Keys keys, uint8_t *d_bitmaps, void *ws, hip
     auto by_block = [&](auto bt) -> int {  // bt: tag type carrying BLOCK
       constexpr int B = decltype(bt)::value;
       if constexpr (std::is_same<Keys, Keys16>::value) {
-        if (p.a.k == 6 && !p.sequential_a && !p.a.dedup)
+        if (p.a.k == 6 && !p.sequential_a && !p.a.dedup) {
+          BuildArgs ah = aa;
+          ah.hot = hot_used = p.hot ? 1u : 0u;
+          if (p.compact) {
+            ah.compact = 1;
+            return go_src(adl_host::lds_limit<bloom_bin16_kernel<B, 6, Src16, DT, true>>,
+                          bloom_bin16_kernel<B, 6, Src16, DT, true>, ah, Src16{keys.keys}, false);
+          }
           return go_src(adl_host::lds_limit<bloom_bin16_kernel<B, 6, Src16, DT>>, bloom_bin16_kernel<B, 6, Src16, DT>,
-                        p.a, Src16{keys.keys}, false);
+                        ah, Src16{keys.keys}, false);
+        }
       }
       if constexpr (std::is_same<Keys, KeysVar>::value) {
         // length-sorted hashing pass, then pass A over the (h1, h2) pairs; the
@@ -1409,7 +1619,7 @@ int launch_binned_dt(const Plan &p, Keys keys, uint8_t *d_bitmaps, void *ws, hip
           auto hv_go = [&](auto lim, auto kern, size_t lds) -> int {
             if (int rc = lim()) return rc;
             hipExtLaunchKernelGGL(kern, dim3(p.total_sc), dim3(kHvBlock), lds, st, ev ? ev[0] : nullptr, nullptr, 0,
-                                  p.a, keys, hp, p.total_sc, ft);
+                                  aa, keys, hp, p.total_sc, ft);
             ADL_HIP_TRY(hipGetLastError());
             return ADL_OK;
           };
@@ -1427,7 +1637,7 @@ int launch_binned_dt(const Plan &p, Keys keys, uint8_t *d_bitmaps, void *ws, hip
           if (rh) return rh;
           // the pair table pays for 16-byte keys only (configs[2]'s keys repeat few pairs:
           // pass B 64 -> 70 us with it)
-          BuildArgs av = p.a;
+          BuildArgs av = aa;
           av.dd_log2 = 0;
           return go_src(adl_host::lds_limit<bloom_bin16_kernel<B, 6, SrcH, DT>>, bloom_bin16_kernel<B, 6, SrcH, DT>,
                         av, SrcH{hp, p.a.C}, true);
@@ -1435,15 +1645,16 @@ int launch_binned_dt(const Plan &p, Keys keys, uint8_t *d_bitmaps, void *ws, hip
       }
       if (p.a.k == 6)
         return go_src(adl_host::lds_limit<bloom_bin_kernel<B, 6, 6, Keys, DT>>, bloom_bin_kernel<B, 6, 6, Keys, DT>,
-                      p.a, keys, false);
+                      aa, keys, false);
       return go_src(adl_host::lds_limit<bloom_bin_kernel<B, 0, kKptMax, Keys, DT>>,
-                    bloom_bin_kernel<B, 0, kKptMax, Keys, DT>, p.a, keys, false);
+                    bloom_bin_kernel<B, 0, kKptMax, Keys, DT>, aa, keys, false);
     };
     const int rc = p.block_a == 1024 ? by_block(std::integral_constant<int, 1024>{})
                                      : by_block(std::integral_constant<int, 512>{});
     if (rc) return rc;
   }
-  BuildArgs ab = p.a;
+  BuildArgs ab = aa;
+  ab.hot = hot_used;
   if (!p.total_chunks) ab.dyn_tiles = 0;  // no pass A ran to reset the queue
   auto go_b = [&](auto lim, auto kern) -> int {
     if (int rc = lim()) return rc;

@@ -303,14 +303,19 @@ int adl_bloom_filter_cache_probe(adl_bloom_filter_cache *c, const char *const *o
     // 1. under the lock: per listed table, the arena range of its filter
     //    `filter` (the all-ones filter when the table is not cached, an empty
     //    range when it has no such filter), its entry pinned and marked used
-    std::vector<uint64_t> be(2 * (size_t)num_tables);
-    std::vector<uint8_t> cached(num_tables);
-    std::vector<adl_bloom_filter_cache::Iter> pinned;
-    pinned.reserve(num_tables);
+    // (per-thread scratch: a single-key Get allocates nothing here)
+    thread_local std::vector<uint64_t> be;
+    thread_local std::vector<uint8_t> cached;
+    thread_local std::vector<adl_bloom_filter_cache::Iter> pinned;
+    thread_local std::string oid_key;
+    be.assign(2 * (size_t)num_tables, 0);
+    cached.assign(num_tables, 0);
+    pinned.clear();
     {
       std::lock_guard<std::mutex> g(c->mu);
       for (uint32_t j = 0; j < num_tables; ++j) {
-        auto it = c->index.find(std::string(oids[j], oid_lens[j]));
+        oid_key.assign(oids[j], oid_lens[j]);
+        auto it = c->index.find(oid_key);
         if (it == c->index.end()) {
           be[j] = 0;
           be[num_tables + j] = kOnesBytes;

@@ -49,16 +49,18 @@ __device__ __forceinline__ uint32_t mix_k(uint32_t k) {
   return k * 0x1b873593u; // :33
 }
 
-// The state update with a mixed block word (src/murmur3_hash.cpp:35-37).
-__device__ __forceinline__ uint32_t mix_h(uint32_t h, uint32_t k) {
-  h ^= k;                 // :35
-  // :36, h*5 + c as shift + 3-input add: an opaque shift keeps the compiler
-  // from fusing it back into a 64-bit v_mad_u64_u32
-  const uint32_t r = rotl_quirk<13>(h);
+// The rest of the state update once the block word is XORed in
+// (src/murmur3_hash.cpp:36): h*5 + c as shift + 3-input add, an opaque shift
+// keeping the compiler from fusing it back into a 64-bit v_mad_u64_u32.
+__device__ __forceinline__ uint32_t mix_s(uint32_t s) {
+  const uint32_t r = rotl_quirk<13>(s);
   uint32_t r4 = r << 2;
   asm("" : "+v"(r4));
   return r4 + r + 0xe6546b64u;
 }
+
+// The state update with a mixed block word (src/murmur3_hash.cpp:35-37).
+__device__ __forceinline__ uint32_t mix_h(uint32_t h, uint32_t k) { return mix_s(h ^ k); }
 
 __device__ __forceinline__ uint32_t mix_block(uint32_t h, uint32_t k) { return mix_h(h, mix_k(k)); }
 
@@ -108,6 +110,33 @@ __device__ __forceinline__ void hash16(uint4 raw, uint32_t &h1, uint32_t &h2) {
   mix_block2(a, b, w3);
   h1 = fmix(a, 16u);
   h2 = fmix(b, 16u);
+}
+
+// Collapsed 16-byte keys.  The last block's rotate (src/murmur3_hash.cpp:5-9,
+// :36) of a negative state s is (s << 13) | (s >> 19, arithmetic) =
+// 0xFFFFF000 | s[30:19]: 12 bits survive.  When both seeds' states are
+// negative there and agree in bits 30..19, the key's two hashes are equal and
+// one of 4 096 values fixed by the algorithm alone (hot_h16); 25 % of random
+// keys do this (SplitMix64, 10 M keys: 2 515 004 of them, all 4 096 indices).
+// Such a key sets exactly the bits (j+1) * hot_h16(i) % m, j < k, whatever
+// its bytes, so a build needs each present index once, not each key.
+__device__ __forceinline__ uint32_t hot_h16(uint32_t i) { return fmix(mix_s(0x80000000u | (i << 19)), 16u); }
+
+// hash16 that also reports the collapse when `en`: hot = true, h1 = the index
+// i (h2 unspecified); otherwise (or !en) h1/h2 as hash16.
+__device__ __forceinline__ void hash16h(uint4 raw, uint32_t &h1, uint32_t &h2, bool &hot, bool en) {
+  const uint32_t w0 = quirk_word(raw.x), w1 = quirk_word(raw.y);
+  const uint32_t w2 = quirk_word(raw.z), w3 = quirk_word(raw.w);
+  uint32_t a = kSeed1, b = kSeed2;
+  mix_block2(a, b, w0);
+  mix_block2(a, b, w1);
+  mix_block2(a, b, w2);
+  const uint32_t kk = mix_k(w3);
+  const uint32_t sa = a ^ kk, sb = b ^ kk;
+  h1 = fmix(mix_s(sa), 16u);
+  h2 = fmix(mix_s(sb), 16u);
+  hot = en && (int32_t)(sa & sb) < 0 && ((sa ^ sb) & 0x7FF80000u) == 0;
+  if (hot) h1 = (sa >> 19) & 0xFFFu;
 }
 
 // Unaligned little-endian 32-bit read of 4 bytes (global or LDS generic pointer).

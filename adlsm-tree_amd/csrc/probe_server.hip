@@ -14,7 +14,9 @@
 //   bell[j] (u32)    request sequence number, written after the slot (release);
 //                    the 64 bells share 256 bytes, so one wave-wide load polls
 //                    every slot
-//   done[j] (64 B)   answers, then the served sequence number (release)
+//   done[j] (64 B)   the served sequence number, the answers and the sequence
+//                    number again, written as ONE 16-byte store: the host
+//                    takes the answers once both copies carry its number
 //
 // The wave polls the bells, copies every pending slot into LDS with one load
 // per lane per slot (one round trip for all of them), hashes each query's key
@@ -65,11 +67,12 @@ struct Slot {
 static_assert(sizeof(Slot) == kSlotBytes, "slot size");
 
 struct Done {
+  uint32_t seq0;
   uint8_t ans[adl_srv::kMaxQ];
-  uint32_t status;
-  uint32_t seq;
+  uint32_t seq1;
   uint8_t pad[64 - adl_srv::kMaxQ - 8];
 };
+static_assert(adl_srv::kMaxQ == 8, "the done line's 16-byte store holds 8 answers");
 static_assert(sizeof(Done) == 64, "done line");
 
 struct Ctl {
@@ -96,7 +99,7 @@ __global__ __launch_bounds__(64) void probe_server_kernel(Area *area, uint64_t i
   __shared__ __attribute__((aligned(16))) uint8_t lslot[kSlots][kSlotBytes];
   __shared__ uint8_t lans[kSlots][adl_srv::kMaxQ];
   const uint32_t lane = threadIdx.x;
-  uint32_t served = __hip_atomic_load(&area->done[lane].seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  uint32_t served = __hip_atomic_load(&area->done[lane].seq1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   const uint64_t t0 = now_ticks();
   uint64_t last = t0;
   for (;;) {
@@ -167,18 +170,18 @@ __global__ __launch_bounds__(64) void probe_server_kernel(Area *area, uint64_t i
       lans[j][q] = hit;
     }
     __syncthreads();
-    // answers, then (after a system-scope release) the sequence numbers
+    // sequence number, answers, sequence number: one 16-byte store per slot
+    // (the mapped memory is not cached on the device, so it goes straight out)
     if (pend) {
-      uint64_t a = 0;
+      uint32_t w1 = 0, w2 = 0;
 #pragma unroll
-      for (uint32_t q = 0; q < adl_srv::kMaxQ; ++q) a |= (uint64_t)lans[lane][q] << (8 * q);
-      __hip_atomic_store(reinterpret_cast<uint64_t *>(area->done[lane].ans), a, __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_SYSTEM);
-      __hip_atomic_store(&area->done[lane].status, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-    if (pend) {
-      __hip_atomic_store(&area->done[lane].seq, bell, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      for (uint32_t q = 0; q < 4; ++q) {
+        w1 |= (uint32_t)lans[lane][q] << (8 * q);
+        w2 |= (uint32_t)lans[lane][q + 4] << (8 * q);
+      }
+      typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+      const u32x4 v = {bell, w1, w2, bell};
+      *reinterpret_cast<u32x4 *>(&area->done[lane]) = v;
       served = bell;
     }
     last = now_ticks();
@@ -333,7 +336,12 @@ int probe(Server *s, const uint8_t *h_keys, const uint64_t *h_offsets, uint32_t 
   const auto t0 = std::chrono::steady_clock::now();
   auto since = [&] { return std::chrono::steady_clock::now() - t0; };
   uint32_t spins = 0;
-  while (__atomic_load_n(&dn->seq, __ATOMIC_ACQUIRE) != seq) {
+  uint8_t a[kMaxQ];
+  for (;;) {
+    if (__atomic_load_n(&dn->seq0, __ATOMIC_ACQUIRE) == seq) {
+      for (uint32_t q = 0; q < kMaxQ; ++q) a[q] = dn->ans[q];
+      if (__atomic_load_n(&dn->seq1, __ATOMIC_ACQUIRE) == seq) break;  // the whole line is this answer
+    }
     __builtin_ia32_pause();
     if (++spins % 4096) continue;
     // not answered yet: a server that exited (idle / life limit) before it saw
@@ -344,9 +352,6 @@ int probe(Server *s, const uint8_t *h_keys, const uint64_t *h_offsets, uint32_t 
     }
     if (since() > std::chrono::seconds(2)) return ADL_ERR_DEVICE;
   }
-  uint8_t a[kMaxQ];
-  for (uint32_t q = 0; q < kMaxQ; ++q) a[q] = dn->ans[q];
-  if (dn->status) return ADL_ERR_DEVICE;
   memcpy(h_out, a, n);
   return ADL_OK;
 }

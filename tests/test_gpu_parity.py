@@ -330,6 +330,48 @@ def test_build_compaction_shape_32_tables(dev, ab, oracle):
         assert np.array_equal(got, oracle.keys2block(oracle.splitmix_keys16(0x5EED + t, n))), t
 
 
+@pytest.mark.parametrize("compact", ["0", "1"])
+def test_build_collapsed_keys_stamped(dev, ab, oracle, golden, monkeypatch, compact):
+    """ADL_BLOOM_HOT=1 (opt-in, round 4): a 16-byte key whose murmur seeds
+    collapse marks its index (one of 4 096) per workgroup and filter instead of
+    binning k positions, and pass B adds the marked indices' bits; with
+    ADL_BLOOM_COMPACT=1 the live keys are also staged densely in LDS.  The
+    10 M reference SHA (7 chunks per workgroup, three builds into the same
+    workspace: each launch pair's stamps carry a new nonce), 1.5 M keys, a
+    segmented build mixing filters of only collapsed keys with ordinary and
+    empty ones, and the 32-table shape (several filters per workgroup)."""
+    monkeypatch.setenv("ADL_BLOOM_HOT", "1")
+    monkeypatch.setenv("ADL_BLOOM_COMPACT", compact)
+    g = golden["appendix_b"]["bitmaps"][5]
+    keys = ab.synth_keys16(g["n"], seed=0x5EED)
+    b = ab.Builder(g["n"], 10)
+    for _ in range(3):
+        bm = b.build(keys).cpu().numpy()
+        assert hashlib.sha256(bm.tobytes()).hexdigest() == g["sha256"]
+    k15 = ab.synth_keys16(1_500_000, seed=0x5EED)
+    assert np.array_equal(ab.build(k15).cpu().numpy(), oracle.keys2block(k15.cpu().numpy()))
+    # filters of collapsed keys only (h1 == h2), ordinary ones and empty ones in one build
+    pool = oracle.splitmix_keys16(0xC011, 400_000)
+    hh = oracle.murmur3_batch(pool)
+    hot = pool[hh[:, 0] == hh[:, 1]]
+    plain = oracle.splitmix_keys16(0xC012, 120_000)
+    parts = [hot[:50_000], plain[:100_000], hot[50_000:50_007], plain[100_000:100_001], hot[:0], hot[60_000:]]
+    kb = np.concatenate([[0], np.cumsum([len(x) for x in parts])]).astype(np.uint64)
+    out, boff, nbytes = ab.build_segmented(dev.from_numpy(np.concatenate(parts)).cuda(), kb)
+    out = out.cpu().numpy()
+    for f, x in enumerate(parts):
+        got = out[int(boff[f]):int(boff[f]) + int(nbytes[f])]
+        if len(x):
+            assert np.array_equal(got, oracle.keys2block(x)), f
+    T, n = 32, 100_000
+    kt = dev.cat([ab.synth_keys16(n, seed=0x5EED + t) for t in range(T)])
+    out, boff, nbytes = ab.build_segmented(kt, np.arange(T + 1, dtype=np.uint64) * n)
+    out = out.cpu().numpy()
+    for t in (0, 5, 31):
+        got = out[int(boff[t]):int(boff[t]) + int(nbytes[t])]
+        assert np.array_equal(got, oracle.keys2block(oracle.splitmix_keys16(0x5EED + t, n))), t
+
+
 @pytest.mark.parametrize("pinned", [False, True])
 def test_build_segmented_host_pipelined(dev, ab, oracle, pinned):
     # adl_bloom_build_segmented: host keys -> pipelined groups -> host bitmaps packed
