@@ -14,9 +14,10 @@
 //   bell[j] (u32)    request sequence number, written after the slot (release);
 //                    the 64 bells share 256 bytes, so one wave-wide load polls
 //                    every slot
-//   done[j] (64 B)   the served sequence number, the answers and the sequence
-//                    number again, written as ONE 16-byte store: the host
-//                    takes the answers once both copies carry its number
+//   done[j] (64 B)   word 0: the served sequence number (a restarted kernel's
+//                    starting point); word 1: the low 24 bits of that number
+//                    above the 8 answer bits.  Both in one 8-byte system-scope
+//                    store; the host takes its answers from word 1 alone
 //
 // The wave polls the bells, copies every pending slot into LDS with one load
 // per lane per slot (one round trip for all of them), hashes each query's key
@@ -67,16 +68,17 @@ struct Slot {
 static_assert(sizeof(Slot) == kSlotBytes, "slot size");
 
 struct Done {
-  uint32_t seq0;
-  uint8_t ans[adl_srv::kMaxQ];
-  uint32_t seq1;
-  uint8_t pad[64 - adl_srv::kMaxQ - 8];
+  uint32_t seq;
+  uint32_t tagged;  // (seq << 8) | answer bits
+  uint32_t pad[14];
 };
-static_assert(adl_srv::kMaxQ == 8, "the done line's 16-byte store holds 8 answers");
 static_assert(sizeof(Done) == 64, "done line");
+static_assert(adl_srv::kMaxQ == 8, "a done word holds 8 answer bits");
 
 struct Ctl {
   uint32_t stop[16];  // replicated: lane l reads stop[l % 16] (a per-lane, vector load)
+  uint32_t alive;     // host: 1 before a launch; kernel: 0 as it returns
+  uint32_t pad[15];
 };
 
 // The shared area, one hipHostMalloc (mapped, coherent): bells, control, done
@@ -99,7 +101,7 @@ __global__ __launch_bounds__(64) void probe_server_kernel(Area *area, uint64_t i
   __shared__ __attribute__((aligned(16))) uint8_t lslot[kSlots][kSlotBytes];
   __shared__ uint8_t lans[kSlots][adl_srv::kMaxQ];
   const uint32_t lane = threadIdx.x;
-  uint32_t served = __hip_atomic_load(&area->done[lane].seq1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  uint32_t served = __hip_atomic_load(&area->done[lane].seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   const uint64_t t0 = now_ticks();
   uint64_t last = t0;
   for (;;) {
@@ -170,22 +172,21 @@ __global__ __launch_bounds__(64) void probe_server_kernel(Area *area, uint64_t i
       lans[j][q] = hit;
     }
     __syncthreads();
-    // sequence number, answers, sequence number: one 16-byte store per slot
-    // (the mapped memory is not cached on the device, so it goes straight out)
+    // the answers: one 8-byte system-scope store (a plain store can sit in the
+    // device's write path while the wave keeps polling: the host then sees it
+    // only when the kernel ends)
     if (pend) {
-      uint32_t w1 = 0, w2 = 0;
+      uint32_t bits = 0;
 #pragma unroll
-      for (uint32_t q = 0; q < 4; ++q) {
-        w1 |= (uint32_t)lans[lane][q] << (8 * q);
-        w2 |= (uint32_t)lans[lane][q + 4] << (8 * q);
-      }
-      typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-      const u32x4 v = {bell, w1, w2, bell};
-      *reinterpret_cast<u32x4 *>(&area->done[lane]) = v;
+      for (uint32_t q = 0; q < adl_srv::kMaxQ; ++q) bits |= (uint32_t)(lans[lane][q] & 1u) << q;
+      const uint64_t v = (uint64_t)bell | ((uint64_t)((bell << 8) | bits) << 32);
+      __hip_atomic_store(reinterpret_cast<uint64_t *>(&area->done[lane]), v, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
       served = bell;
     }
     last = now_ticks();
   }
+  if (lane == 0) __hip_atomic_store(&area->ctl.alive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 }  // namespace
@@ -203,6 +204,7 @@ struct Server {
   std::mutex slot_mu[kSlots];
   uint32_t seq[kSlots] = {};
   std::atomic<uint32_t> next_slot{0};
+  uint64_t id = 0;  // unique per server of this process (a thread's slot is per server)
   uint64_t idle_ticks = 0, life_ticks = 0;
 };
 
@@ -240,6 +242,7 @@ int ensure_running(Server *s) {
     }
   }
   set_stop(s, 0);
+  __atomic_store_n(&s->host->ctl.alive, 1u, __ATOMIC_SEQ_CST);
   hipExtLaunchKernelGGL(probe_server_kernel, dim3(1), dim3(64), 0, s->stream, nullptr, s->exited, 0, s->dev,
                         s->idle_ticks, s->life_ticks);
   if (hipGetLastError() != hipSuccess) return ADL_ERR_DEVICE;
@@ -260,6 +263,8 @@ Server *create() {
     delete s;
     return nullptr;
   };
+  static std::atomic<uint64_t> next_id{1};
+  s->id = next_id.fetch_add(1);
   if (hipGetDevice(&s->device) != hipSuccess) return fail();
   void *d = nullptr;
   if (hipHostMalloc((void **)&s->host, sizeof(Area), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
@@ -311,9 +316,14 @@ int probe(Server *s, const uint8_t *h_keys, const uint64_t *h_offsets, uint32_t 
           const uint64_t *range, uint32_t k, uint8_t *h_out) {
   const uint64_t key_bytes = h_offsets ? h_offsets[n] - h_offsets[0] : n * (uint64_t)key_stride;
   if (!s || !eligible(n, key_bytes)) return ADL_ERR_INVALID_ARG;
-  // a slot per thread (round-robin); threads beyond kSlots share one in turn
-  thread_local uint32_t my = ~0u;
-  if (my == ~0u) my = s->next_slot.fetch_add(1) % kSlots;
+  // a slot per thread and server (round-robin); threads beyond kSlots share
+  // one in turn.  A thread remembers its slot for the server it used last.
+  thread_local uint64_t my_server = 0;
+  thread_local uint32_t my = 0;
+  if (my_server != s->id) {
+    my = s->next_slot.fetch_add(1) % kSlots;
+    my_server = s->id;
+  }
   std::lock_guard<std::mutex> slot_guard(s->slot_mu[my]);
   Slot &sl = s->host->slot[my];
   sl.n = (uint32_t)n;
@@ -328,7 +338,9 @@ int probe(Server *s, const uint8_t *h_keys, const uint64_t *h_offsets, uint32_t 
   memcpy(sl.keys, h_keys + (h_offsets ? h_offsets[0] : 0), key_bytes);
   const uint32_t seq = ++s->seq[my] == 0 ? ++s->seq[my] : s->seq[my];  // never 0 (the initial done)
   __atomic_store_n(&s->host->bell[my], seq, __ATOMIC_SEQ_CST);
-  {
+  // a running kernel keeps alive at 1 (cheaper than querying its event every
+  // call); one that is just exiting is caught by the 50 us check below
+  if (!__atomic_load_n(&s->host->ctl.alive, __ATOMIC_ACQUIRE)) {
     std::lock_guard<std::mutex> g(s->launch_mu);
     if (int rc = ensure_running(s)) return rc;
   }
@@ -336,11 +348,12 @@ int probe(Server *s, const uint8_t *h_keys, const uint64_t *h_offsets, uint32_t 
   const auto t0 = std::chrono::steady_clock::now();
   auto since = [&] { return std::chrono::steady_clock::now() - t0; };
   uint32_t spins = 0;
-  uint8_t a[kMaxQ];
+  uint32_t bits = 0;
   for (;;) {
-    if (__atomic_load_n(&dn->seq0, __ATOMIC_ACQUIRE) == seq) {
-      for (uint32_t q = 0; q < kMaxQ; ++q) a[q] = dn->ans[q];
-      if (__atomic_load_n(&dn->seq1, __ATOMIC_ACQUIRE) == seq) break;  // the whole line is this answer
+    const uint32_t w = __atomic_load_n(&dn->tagged, __ATOMIC_ACQUIRE);
+    if ((w >> 8) == (seq & 0xFFFFFFu)) {
+      bits = w & 0xFFu;
+      break;
     }
     __builtin_ia32_pause();
     if (++spins % 4096) continue;
@@ -352,7 +365,7 @@ int probe(Server *s, const uint8_t *h_keys, const uint64_t *h_offsets, uint32_t 
     }
     if (since() > std::chrono::seconds(2)) return ADL_ERR_DEVICE;
   }
-  memcpy(h_out, a, n);
+  for (uint64_t q = 0; q < n; ++q) h_out[q] = (uint8_t)((bits >> q) & 1u);
   return ADL_OK;
 }
 

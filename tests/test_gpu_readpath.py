@@ -287,7 +287,7 @@ def _pack(keys):
 
 @pytest.mark.parametrize("bpk", [3, 10, 44])
 def test_probe_server_single_keys_vs_oracle(dev, ab, oracle, monkeypatch, bpk):
-    """Batches of 1..8 queries (keys of 0..320 bytes, several tables, an
+    """Batches of 1..8 queries (keys of 0..288 bytes, several tables, an
     uncached table, a filter index the block does not have) through the
     resident server equal the oracle and the launched probe."""
     T = 3
@@ -307,7 +307,7 @@ def test_probe_server_single_keys_vs_oracle(dev, ab, oracle, monkeypatch, bpk):
             if t < T and rng.integers(0, 2):
                 qs.append(tabs[t][0][int(rng.integers(0, 3000))])  # a member
             else:
-                qs.append(rng.integers(0, 256, int(rng.integers(0, 321 // n)), dtype=np.uint8).tobytes())
+                qs.append(rng.integers(0, 256, int(rng.integers(0, 289 // n)), dtype=np.uint8).tobytes())
         data, offs = _pack(qs)
         want = np.array([1 if t == T else
                          int(oracle.probe(data, tabs[t][2], offsets=offs[i:i + 2].copy(), bits_per_key=bpk)[0])
