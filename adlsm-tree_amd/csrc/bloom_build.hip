@@ -93,6 +93,8 @@ struct BuildArgs {
   uint32_t dedup;      // skip a key equal to its predecessor in the same filter (ADL_BLOOM_SKIP_ADJACENT_DUPLICATES)
   uint32_t scan1;      // pass A: one-barrier tile-count scan (ADL_BLOOM_SCAN1)
   uint32_t hv_keys;    // keys per hash_var_kernel run (ADL_BLOOM_HV_KEYS)
+  uint32_t hv_split;   // hash_var_kernel: a run's longest groups hashed by two waves, one seed each (ADL_BLOOM_HV_SPLIT)
+  uint32_t pad_hv_;
   uint32_t dd_log2;    // bloom_bin16_kernel: log2 slots of the (h1, h2) table that skips repeated hashes
                        // (0: off; ADL_BLOOM_HASH_DEDUP)
   uint32_t dd_mode;    // 1: every key claims its (h1, h2); 2: keys with h1 == h2 claim h1 (ADL_BLOOM_DD_MODE)
@@ -667,8 +669,37 @@ __global__ __launch_bounds__(kHvBlock) void hash_var_kernel(BuildArgs a, KeysVar
   // groups that set the workgroup's end, and the short ones fill in behind.
   // (A queue handing each free wave the next group measured the same: the
   // longest group alone sets the end.)
-  for (uint32_t gi = wave; gi < groups; gi += NW) {
-    const uint32_t g = groups - 1 - gi;
+  // The `sp` longest groups first, each split between two waves by seed
+  // (waves 2q and 2q+1 take group groups-1-q): their keys set the workgroup's
+  // end, and one seed's chain is about three quarters of both seeds' work.
+  // The other groups follow, longest first, starting with the waves that
+  // split the shorter of them.
+  const uint32_t sp = min(min(a.hv_split, NW / 2), groups);
+  if (wave < 2 * sp) {
+    const uint32_t g = groups - 1 - wave / 2, sd = wave & 1u;
+    const uint32_t s = g * kWave + lane;
+    if (s < cnt) {
+      uint32_t len = s_len[s];
+      const uint32_t r = s_rel[s];
+      uint32_t h;
+      if (len < 0xffffu && (uint64_t)r + len <= sbytes) {
+        h = hash_lds1(stage, r, len, sd ? kSeed2 : kSeed1);
+      } else {
+        uint64_t k0 = base16 + r;
+        if (len == 0xffffu) {
+          k0 = keys.offs[kb + r];
+          len = (uint32_t)(keys.offs[kb + r + 1] - k0);
+        }
+        uint32_t h1, h2;
+        hash_bytes(keys.keys + k0, len, kSeed1, kSeed2, h1, h2);
+        h = sd ? h2 : h1;
+      }
+      reinterpret_cast<uint32_t *>(out + s)[sd] = h;
+    }
+  }
+  const uint32_t rot = (wave + NW - 2 * sp) % NW;  // waves past the split ones start phase 2
+  for (uint32_t gi = rot; gi + sp < groups; gi += NW) {
+    const uint32_t g = groups - 1 - sp - gi;
     const uint32_t s = g * kWave + lane;
     if (s >= cnt) continue;
     uint32_t len = s_len[s];
@@ -1445,6 +1476,7 @@ int make_plan(const uint64_t *counts, uint32_t nf, int32_t bpk, Plan &p) {
   {
     const uint32_t hk = env_u32("ADL_BLOOM_HV_KEYS", 512);
     p.a.hv_keys = hk <= 256 ? 256 : hk <= 512 ? 512 : hk <= 1024 ? 1024 : 2048;
+    p.a.hv_split = env_u32("ADL_BLOOM_HV_SPLIT", 0);
   }
 #ifdef ADL_BLOOM_STAMPS
   p.a.exp = env_u32("ADL_BLOOM_EXP", 0);  // diagnostics build only

@@ -225,6 +225,42 @@ __device__ __forceinline__ void hash_lds(const uint32_t *stage, uint32_t off, ui
   hb = fmix(b, len);
 }
 
+// One seed of a key staged in LDS (hash_lds with a single state): the
+// var-len hashing pass splits a run's longest keys between two waves, one
+// seed each.
+__device__ __forceinline__ uint32_t hash_lds1(const uint32_t *stage, uint32_t off, uint32_t len, uint32_t seed) {
+  uint32_t a = seed;
+  const uint32_t nblk = len >> 2, sh = off & 3u;
+  uint32_t wi = off >> 2;
+  uint32_t i = 0;
+  const uint2 *s2 = reinterpret_cast<const uint2 *>(stage);
+  const bool odd = (wi & 1u) != 0;
+  uint2 p0 = s2[wi >> 1];
+  uint32_t lo = odd ? p0.y : p0.x;
+  uint32_t pi = wi >> 1;
+  for (; i + 4 <= nblk; i += 4) {
+    const uint2 p1 = s2[pi + 1], p2 = s2[pi + 2];
+    const uint32_t w[4] = {odd ? p1.x : p0.y, odd ? p1.y : p1.x, odd ? p2.x : p1.y, odd ? p2.y : p2.x};
+#pragma unroll
+    for (int u = 0; u < 4; ++u) a = mix_block(a, quirk_word(__builtin_amdgcn_alignbyte(w[u], u ? w[u - 1] : lo, sh)));
+    lo = w[3];
+    p0 = p2;
+    pi += 2;
+    wi += 4;
+  }
+  for (; i < nblk; ++i) {
+    const uint32_t hi = stage[++wi];
+    a = mix_block(a, quirk_word(__builtin_amdgcn_alignbyte(hi, lo, sh)));
+    lo = hi;
+  }
+  const uint32_t rem = len & 3u;
+  if (rem) {
+    const uint32_t raw = __builtin_amdgcn_alignbyte(stage[wi + 1], lo, sh);
+    a ^= mix_tail_k(tail_word(raw, rem));
+  }
+  return fmix(a, len);
+}
+
 // h % m for a launch-constant divisor 2 <= m < 2^31 (Granlund-Montgomery
 // round-up method, exact for every 32-bit numerator): q = (t + ((h-t)>>1)) >> (l-1),
 // t = mulhi(h, magic), l = ceil(log2 m).  A power of two m = 2^l gets magic = 1

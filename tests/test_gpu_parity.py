@@ -228,6 +228,24 @@ def test_build_varlen_hashing_run_sizes(dev, ab, oracle, monkeypatch, hv_keys):
     assert np.array_equal(bm, oracle.keys2block(data.cpu().numpy(), offs.cpu().numpy().view(np.uint64)))
 
 
+@pytest.mark.parametrize("split", ["0", "1", "2"])
+def test_build_varlen_seed_split(dev, ab, oracle, monkeypatch, split):
+    """ADL_BLOOM_HV_SPLIT: a hashing run's longest groups hashed by two waves,
+    one seed each (hash_lds1), the rest as before; runs with fewer groups than
+    the split (short filters), keys past the staged bytes and long keys."""
+    monkeypatch.setenv("ADL_BLOOM_HV_SPLIT", split)
+    data, offs = ab.synth_varlen(150_001, seed=91 + int(split))
+    bm = ab.build(data, offs).cpu().numpy()
+    assert np.array_equal(bm, oracle.keys2block(data.cpu().numpy(), offs.cpu().numpy().view(np.uint64)))
+    rng = np.random.default_rng(int(split))
+    for n, lo, hi in ((1, 0, 40), (70, 0, 300), (1000, 200, 700), (5000, 0, 90)):
+        lens = rng.integers(lo, hi + 1, n)
+        o = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+        kb = rng.integers(0, 256, int(o[-1]) + 16, dtype=np.uint8)
+        got = ab.build(dev.from_numpy(kb).cuda(), dev.from_numpy(o.view(np.int64)).cuda()).cpu().numpy()
+        assert np.array_equal(got, oracle.keys2block(kb, o)), (n, lo, hi)
+
+
 @pytest.mark.parametrize("mode", ["1", "2"])
 def test_build_pair_table_modes(dev, ab, oracle, monkeypatch, mode):
     # ADL_BLOOM_DD_MODE 1: every key claims its (h1, h2); 2 (default): keys with
