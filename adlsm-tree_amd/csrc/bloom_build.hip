@@ -60,6 +60,9 @@ constexpr uint32_t kHistMax = 2049; // tiles per filter + 1 (m < 2^31, TL >= ...
 constexpr uint32_t kMinTileLog2 = 10;
 constexpr uint32_t kMaxTileLog2 = 20;     // 128 KiB LDS tile
 constexpr uint32_t kTargetWorkgroups = 512;
+constexpr uint32_t kFewTiles = 256;       // tiles per filter below which smaller tiles are taken
+constexpr uint32_t kMinRun = 64;          // ... while a chunk's run per tile stays this long (positions)
+constexpr uint32_t kChunkEst = 5500;      // keys per pass-A chunk (k = 6), for that estimate
 constexpr uint32_t kHotN = 4096;          // collapsed-key indices per filter (hash16h)
 
 struct FilterDesc {
@@ -1105,8 +1108,11 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin16_kernel(BuildArgs a, Src key
 // while the current stage is ds_or_b32'd into the LDS tile.  The rare longer
 // segments (hot tiles) finish in a 4-deep unrolled loop.  The finished tile's
 // 16-byte stores drain while the next tile is zeroed.
-template <int D, bool DT>
-__global__ __launch_bounds__(kBlockB) void bloom_tile_kernel(BuildArgs a,
+// HOT: pass A stamped collapsed keys (a.hot), whose bits this pass adds.
+// OCC: workgroups per CU the kernel is compiled for (2: at most 64 VGPRs, for
+// tiles whose LDS leaves room for two; ADL_BLOOM_B_OCC).
+template <int D, bool DT, bool HOT = false, int OCC = 1>
+__global__ __launch_bounds__(kBlockB, 4 * OCC) void bloom_tile_kernel(BuildArgs a,
                                                              const uint32_t *__restrict__ pos_ws,
                                                              const uint32_t *__restrict__ table_ws,
                                                              uint8_t *__restrict__ bitmaps,
@@ -1116,12 +1122,15 @@ __global__ __launch_bounds__(kBlockB) void bloom_tile_kernel(BuildArgs a,
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   const int tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid / kWave;
   constexpr int NWAVES = kBlockB / kWave;
-  constexpr int RPT = kSegBatch / kBlockB;  // table entries per thread per batch
+  // segment descriptors staged per batch (half at two workgroups per CU, so
+  // a 2^19-bit tile and its batch fit twice in a CU's LDS)
+  constexpr int SEGB = OCC == 2 ? kSegBatch / 2 : kSegBatch;
+  constexpr int RPT = SEGB / kBlockB;  // table entries per thread per batch
   const uint32_t TL = a.TL;
   const uint32_t tile_words = 1u << (TL - 5);
   uint32_t *tile = lds;                                      // 2^TL bits
-  uint2 *seg = reinterpret_cast<uint2 *>(lds + tile_words);  // kSegBatch {start word, length}
-  uint32_t *qs = lds + tile_words + 2 * kSegBatch;           // tile-queue broadcast (2 words)
+  uint2 *seg = reinterpret_cast<uint2 *>(lds + tile_words);  // SEGB {start word, length}
+  uint32_t *qs = lds + tile_words + 2 * SEGB;                // tile-queue broadcast (2 words)
 
   auto fetch_rows = [&](uint32_t wg, uint32_t wb, uint32_t (&rs)[RPT], uint32_t (&re)[RPT]) {
     const auto &d = FT::at(a, ft, FT::of_tile(a, ft, wg));
@@ -1176,7 +1185,7 @@ __global__ __launch_bounds__(kBlockB) void bloom_tile_kernel(BuildArgs a,
 
   // Collapsed keys (a.hot): thread t holds the positions (j+1)*hot_h16(i) % m
   // of indices i = t + q*kBlockB, computed once per divisor m.
-  constexpr int kHQ = (int)(kHotN / kBlockB), kHotK = 6;  // pass A's collapsed-key path has k == 6
+  constexpr int kHQ = HOT ? (int)(kHotN / kBlockB) : 1, kHotK = 6;  // pass A's collapsed-key path has k == 6
   uint32_t hpos[kHQ][kHotK];
   uint32_t hot_m = 0;  // m that hpos holds positions for (0: none yet)
 
@@ -1190,7 +1199,7 @@ __global__ __launch_bounds__(kBlockB) void bloom_tile_kernel(BuildArgs a,
     if (a.dyn_tiles && tid == 0) qs[1] = atomicAdd(tile_queue, 1u);
     __syncthreads();  // next tile index published
     STAMP(0);
-    if (a.hot) {  // the bits of the collapsed keys pass A stamped for this filter
+    if constexpr (HOT) {  // the bits of the collapsed keys pass A stamped for this filter
       if (d.mod.m != hot_m) {
         hot_m = d.mod.m;
 #pragma unroll
@@ -1212,8 +1221,8 @@ __global__ __launch_bounds__(kBlockB) void bloom_tile_kernel(BuildArgs a,
     // an empty filter (no chunks) has no batch to prefetch the next tile from
     if (W == 0 && next < total_tiles) fetch_rows(next, 0, pre_s, pre_e);
 
-    for (uint32_t wb = 0; wb < W; wb += kSegBatch) {
-      const uint32_t nw = min((uint32_t)kSegBatch, W - wb);
+    for (uint32_t wb = 0; wb < W; wb += SEGB) {
+      const uint32_t nw = min((uint32_t)SEGB, W - wb);
       uint32_t rs[RPT], re[RPT];
       if (wb == 0) {
 #pragma unroll
@@ -1228,7 +1237,7 @@ __global__ __launch_bounds__(kBlockB) void bloom_tile_kernel(BuildArgs a,
       }
       __syncthreads();  // segment list ready
       STAMP(1);
-      if (wb + kSegBatch >= W && next < total_tiles) fetch_rows(next, 0, pre_s, pre_e);
+      if (wb + SEGB >= W && next < total_tiles) fetch_rows(next, 0, pre_s, pre_e);
 
       const uint32_t Q = nw > (uint32_t)wave ? (nw - wave + NWAVES - 1) / NWAVES : 0;
       struct Stage {
@@ -1367,6 +1376,7 @@ struct Plan {
   bool compact = false;    // with hot: pass A compacts the live keys (ADL_BLOOM_COMPACT)
   uint32_t total_chunks = 0, total_tiles = 0, total_sc = 0;
   uint32_t grid_a = 0, grid_b = 0;  // persistent grids
+  uint32_t occ_b = 1;               // pass-B workgroups per CU (ADL_BLOOM_B_OCC)
   uint32_t block_a = 512;             // pass A threads per workgroup
   uint32_t depth = kDepthB;           // pass B descriptors per step
   bool sequential_a = false;          // ADL_BLOOM_SEQ_A=1: the unpipelined pass A (A/B tuning)
@@ -1408,10 +1418,21 @@ int make_plan(const uint64_t *counts, uint32_t nf, int32_t bpk, Plan &p) {
     return t;
   };
   while (TL > kMinTileLog2 && tiles_at(TL, false) < kTargetWorkgroups) --TL;
+  // Filters of a few tiles each (configs[3]'s 1 M-key tables: 77 tiles of
+  // 2^20 bits): smaller tiles, down to 2^18 bits, while a filter has fewer
+  // than kFewTiles and a chunk's run per tile stays long (about k*C / tiles
+  // positions >= kMinRun).  More tile counters take the contention off pass
+  // A's atomics, and such tiles leave LDS for two pass-B workgroups per CU
+  // (below).  Measured on configs[3]: 3.66-3.68 ms at 2^18 bits with two
+  // per CU, 4.06-4.11 at 2^20 (profiles/r04/ab_tile_size_occ.log).
+  bool tl_set = false;
   if (const char *e = getenv("ADL_BLOOM_TILE_LOG2")) {  // tuning override
     const int v = atoi(e);
-    if (v >= (int)kMinTileLog2 && v <= (int)kMaxTileLog2) TL = (uint32_t)v;
+    if (v >= (int)kMinTileLog2 && v <= (int)kMaxTileLog2) TL = (uint32_t)v, tl_set = true;
   }
+  if (!tl_set && k == 6)
+    while (TL > 18 && tiles_at(TL, true) < kFewTiles && (uint64_t)k * kChunkEst >= kMinRun * tiles_at(TL - 1, true))
+      --TL;
   while (TL < kMaxTileLog2 && tiles_at(TL, true) + 1 > kHistMax) ++TL;
   const uint32_t hist_words = (uint32_t)adl_host::round_up(tiles_at(TL, true) + 1, 4);
 
@@ -1538,7 +1559,28 @@ int make_plan(const uint64_t *counts, uint32_t nf, int32_t bpk, Plan &p) {
   p.block_a = block_a;
   p.depth = env_u32("ADL_BLOOM_DEPTH", kDepthB);
   p.sequential_a = env_flag("ADL_BLOOM_SEQ_A", 0) != 0;
-  p.grid_b = std::min<uint32_t>(p.total_tiles, cus);
+  // Two pass-B workgroups per CU (64-VGPR kernels, half the segment batch)
+  // when the tile leaves room for two in LDS and the runs per tile are long:
+  // more waves to hide the gathers.  On the headline's 2^20-bit tiles it
+  // does not fit; forced at 2^19 there it is slower (short runs: 101 vs 68
+  // us).  ADL_BLOOM_B_OCC = 1 / 2 overrides.
+  {
+    const size_t lds2 = (size_t)((1u << (TL - 5)) + kSegBatch + 4) * 4;
+    const uint32_t want = env_u32("ADL_BLOOM_B_OCC", 0);
+    const bool long_runs = (uint64_t)k * C >= (uint64_t)kMinRun * tiles_at(TL, true);
+    bool two = want == 2 || (want == 0 && long_runs);
+    // (the stamped-keys pass B keeps one per CU: its index tables need the registers)
+    two = two && lds2 <= 80 * 1024 && !p.hot;
+    p.occ_b = two ? 2 : 1;
+    if (two) {
+      p.lds_b = lds2;
+      if (!getenv("ADL_BLOOM_DEPTH")) p.depth = 4;  // measured best at two per CU
+    }
+  }
+  p.grid_b = std::min<uint32_t>(p.total_tiles, p.occ_b * cus);
+  if (adl_host::env_on("ADL_BLOOM_DEBUG", false))
+    fprintf(stderr, "adl_bloom plan: filters %u, tile 2^%u bits, tiles %u, C %u, chunks %u, pass B %u per CU, depth %u\n",
+            nf, TL, p.total_tiles, C, p.total_chunks, p.occ_b, p.depth);
   return ADL_OK;
 }
 
@@ -1696,6 +1738,14 @@ int launch_binned_dt(const Plan &p, Keys keys, uint8_t *d_bitmaps, void *ws, hip
     ADL_HIP_TRY(hipGetLastError());
     return ADL_OK;
   };
+  if (ab.hot) return go_b(adl_host::lds_limit<bloom_tile_kernel<8, DT, true>>, bloom_tile_kernel<8, DT, true>);
+  if (p.occ_b == 2) {
+    if (p.depth <= 4)
+      return go_b(adl_host::lds_limit<bloom_tile_kernel<4, DT, false, 2>>, bloom_tile_kernel<4, DT, false, 2>);
+    if (p.depth <= 6)
+      return go_b(adl_host::lds_limit<bloom_tile_kernel<6, DT, false, 2>>, bloom_tile_kernel<6, DT, false, 2>);
+    return go_b(adl_host::lds_limit<bloom_tile_kernel<8, DT, false, 2>>, bloom_tile_kernel<8, DT, false, 2>);
+  }
   if (p.depth <= 4) return go_b(adl_host::lds_limit<bloom_tile_kernel<4, DT>>, bloom_tile_kernel<4, DT>);
   if (p.depth <= 6) return go_b(adl_host::lds_limit<bloom_tile_kernel<6, DT>>, bloom_tile_kernel<6, DT>);
   if (p.depth <= 8) return go_b(adl_host::lds_limit<bloom_tile_kernel<8, DT>>, bloom_tile_kernel<8, DT>);
