@@ -37,6 +37,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <cmath>
 #include <random>
 #include <mutex>
 #include <type_traits>
@@ -64,6 +65,7 @@ constexpr uint32_t kFewTiles = 256;       // tiles per filter below which smalle
 constexpr uint32_t kMinRun = 64;          // ... while a chunk's run per tile stays this long (positions)
 constexpr uint32_t kChunkEst = 5500;      // keys per pass-A chunk (k = 6), for that estimate
 constexpr uint32_t kHotN = 4096;          // collapsed-key indices per filter (hash16h)
+constexpr uint32_t kClaimTiles = 8;       // claim layout by default only up to this many tiles per filter
 
 struct FilterDesc {
   uint64_t key_begin;   // first key (index into the key set)
@@ -97,8 +99,12 @@ struct BuildArgs {
   uint32_t scan1;      // pass A: one-barrier tile-count scan (ADL_BLOOM_SCAN1)
   uint32_t hv_keys;    // keys per hash_var_kernel run (ADL_BLOOM_HV_KEYS)
   uint32_t hv_split;   // hash_var_kernel: a run's longest groups hashed by two waves, one seed each (ADL_BLOOM_HV_SPLIT)
-  uint32_t pad_hv_;
-  uint32_t dd_log2;    // bloom_bin16_kernel: log2 slots of the (h1, h2) table that skips repeated hashes
+  // Claim layout (ADL_BLOOM_CLAIM; bloom_bin16_kernel<..., CL> and the pass B
+  // after it): a chunk region gives each of a filter's T tiles tcap = (cap / T)
+  // & ~3 fixed slots, a position takes its slot with one ds_add_rtn (no count
+  // pass, no scan), and a (tile, chunk) table entry is (start << 16) | length.
+  uint32_t claim;
+  uint32_t dd_log2;   // bloom_bin16_kernel: log2 slots of the (h1, h2) table that skips repeated hashes
                        // (0: off; ADL_BLOOM_HASH_DEDUP)
   uint32_t dd_mode;    // 1: every key claims its (h1, h2); 2: keys with h1 == h2 claim h1 (ADL_BLOOM_DD_MODE)
   uint32_t var_hash;   // variable-length keys: length-sorted hashing pass + pass A over (h1, h2) (ADL_BLOOM_VAR_HASH)
@@ -773,15 +779,24 @@ struct SrcH {
 //   prefetch keys of c+2
 // so the murmur work hides under the scatter's LDS latency and the position
 // stores drain under the next count.
-template <int BLOCK, int K, class Src, bool DT, bool CMP = false>
+//
+// CL (claim layout, a.claim): every position claims a slot of its tile's
+// fixed share of the chunk region with one ds_add_rtn, so the count pass, the
+// scan and two barriers go; two counter arrays alternate by chunk parity (the
+// store phase zeroes the other one).  A chunk in which some tile overflows its
+// share (rare: the share is the mean plus several standard deviations) is
+// counting-sorted exactly as above from the positions still in registers,
+// and its table entries describe the dense runs instead.
+template <int BLOCK, int K, class Src, bool DT, bool CMP = false, bool CL = false>
 __global__ __launch_bounds__(BLOCK) void bloom_bin16_kernel(BuildArgs a, Src keys,
                                                               uint32_t *__restrict__ pos_ws,
                                                               uint32_t *__restrict__ table_ws,
                                                               uint32_t total_chunks, uint32_t *__restrict__ tile_queue,
                                                               FilterTable ft) {
   using FT = Filt<DT>;
+  static_assert(!(CMP && CL), "live-key compaction and the claim layout do not combine");
   constexpr int KPT = 6;                    // keys per thread (C <= 6 * BLOCK)
-  constexpr int VPT = (K * KPT + 3) / 4;    // 16-byte stores per thread per chunk, at most
+  constexpr int VPT = (K * KPT + 3) / 4;    // 16-byte stores per thread per chunk, at most (CL: cap <= 4 * VPT * BLOCK)
   constexpr int SPI = (VPT + KPT - 1) / KPT;  // of those, per count iteration
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   const int tid = threadIdx.x;
@@ -791,8 +806,12 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin16_kernel(BuildArgs a, Src key
   const uint32_t tmask = (1u << TL) - 1u;
   uint32_t *hist = lds;                        // T+1 counters, later cursors
   uint32_t *scratch = lds + a.hist_words;      // scan scratch
-  uint32_t *lpos = lds + a.hist_words + 32;    // K*C sorted tile offsets
+  uint32_t *lpos = lds + a.hist_words + 32;    // K*C sorted tile offsets (CL: the cap-word region)
   const uint4 *src4 = reinterpret_cast<const uint4 *>(lpos);
+  // CL: the second counter array and the two overflow flags follow the region
+  uint32_t *hist2 = lpos + a.cap;
+  uint32_t *oflag = hist2 + a.hist_words;
+  uint32_t *after = CL ? oflag + 4 : lpos + K * C;  // collapsed-key masks, pair table
 
   const uint32_t G = gridDim.x;
   const uint32_t slot =
@@ -837,6 +856,8 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin16_kernel(BuildArgs a, Src key
   }
   fetch(min(slot + G, total_chunks - 1), raw);
   for (uint32_t i = tid; i < a.hist_words; i += BLOCK) hist[i] = 0;
+  if constexpr (CL)
+    for (uint32_t i = tid; i < a.hist_words + 4; i += BLOCK) hist2[i] = 0;  // and the flags
 
   // Repeated hashes.  The reference's murmur variant collapses: rotations with
   // an arithmetic shift and sign-extended bytes leave SplitMix keys only ~69 %
@@ -852,8 +873,8 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin16_kernel(BuildArgs a, Src key
   // With collapsed keys on, the first 2 * kHotN/32 words of that area are this
   // workgroup's masks of the indices it met in its current and next filter
   // (hpar selects the current one), and the pair table follows.
-  uint32_t *hmask = lpos + K * C;
-  unsigned long long *dtab = reinterpret_cast<unsigned long long *>(lpos + K * C + (hot_on ? 2 * kHotN / 32 : 0));
+  uint32_t *hmask = after;
+  unsigned long long *dtab = reinterpret_cast<unsigned long long *>(after + (hot_on ? 2 * kHotN / 32 : 0));
   uint32_t *dtab32 = reinterpret_cast<uint32_t *>(dtab);
   constexpr unsigned long long kEmpty = ~0ull;
   if (dd)
@@ -912,6 +933,7 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin16_kernel(BuildArgs a, Src key
 
   uint4 *pdst = dummy4;  // deferred store of the previous chunk
   uint32_t ptotal = 0;
+  uint32_t par = 0;  // CL: counter array / overflow flag of this chunk
   STAMP_DECL
   for (uint32_t wg = slot; wg < total_chunks; wg += G) {
     const int fcur = FT::of_chunk(a, ft, wg);
@@ -920,6 +942,9 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin16_kernel(BuildArgs a, Src key
     const uint32_t cnt = min(C, d.n - w * C);
     const uint32_t T = d.tiles;
     const FastMod mod = d.mod;
+    uint32_t *hcur = hist, *hoth = hist2;
+    if (CL && par) hcur = hist2, hoth = hist;
+    const uint32_t tcap = CL ? (a.cap / T) & ~3u : 0u;  // slots per tile (the plan keeps it >= 4)
     __syncthreads();  // hist cleared; the previous scatter is complete in lpos; the live keys staged
     STAMP(0);
 
@@ -983,10 +1008,11 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin16_kernel(BuildArgs a, Src key
 #pragma unroll
           for (int j = 0; j < K; ++j) pos[i][j] = (h1[i] + (uint32_t)j * h2[i]) >> 3;
 #endif
+        if constexpr (!CL)
 #pragma unroll
-        for (int j = 0; j < K; ++j) atomicAdd(&hist[pos[i][j] >> TL], 1u);
+          for (int j = 0; j < K; ++j) atomicAdd(&hist[pos[i][j] >> TL], 1u);
       }
-      if constexpr (!CMP) {
+      if constexpr (!CMP && !CL) {
 #pragma unroll
         for (int sv = i * SPI; sv < (i + 1) * SPI && sv < VPT; ++sv) {
           const uint32_t v = tid + sv * BLOCK;
@@ -998,37 +1024,51 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin16_kernel(BuildArgs a, Src key
         }
       }
     }
-    if constexpr (!CMP) {
+    if constexpr (!CMP && !CL) {
       const bool ok = (uint32_t)tid < (ptotal & 3u);
       *(ok ? reinterpret_cast<uint32_t *>(pdst) + pvec * 4 + tid : dummy) = lpos[ok ? pvec * 4 + tid : 0u];
     }
-    __syncthreads();  // counts complete; the previous chunk's LDS copy is read out
-    STAMP(1);
-
-    const uint32_t total = a.scan1 ? block_excl_scan_array_1b<BLOCK>(hist, T + 1, scratch)
-                                   : block_excl_scan_array<BLOCK>(hist, T + 1, scratch);
-    STAMP(2);
     uint32_t *tab = table_ws + d.table_base;
+    uint32_t total = 0;
+    if constexpr (!CL) {
+      __syncthreads();  // counts complete; the previous chunk's LDS copy is read out
+      STAMP(1);
+
+      total = a.scan1 ? block_excl_scan_array_1b<BLOCK>(hist, T + 1, scratch)
+                      : block_excl_scan_array<BLOCK>(hist, T + 1, scratch);
+      STAMP(2);
 #pragma unroll
-    for (int r = 0; r < TPT; ++r) {
-      const uint32_t t = tid + r * BLOCK;
-      const bool ok = t <= T;
-      *(ok ? tab + (uint64_t)t * d.chunks + w : dummy) = hist[ok ? t : 0u];
+      for (int r = 0; r < TPT; ++r) {
+        const uint32_t t = tid + r * BLOCK;
+        const bool ok = t <= T;
+        *(ok ? tab + (uint64_t)t * d.chunks + w : dummy) = hist[ok ? t : 0u];
+      }
+      __syncthreads();
+      STAMP(3);
     }
-    __syncthreads();
-    STAMP(3);
 
     // scatter(c) + hash(c+1) (its keys arrived during the previous chunk;
     // lanes past the end hash a clamped key and never use the result)
     uint32_t hotn = 0;
+    bool ovf = false;  // CL: a position found its tile's slots taken
 #pragma unroll
     for (int i = 0; i < KPT; ++i) {
       if ((live >> i) & 1u) {
         uint32_t sl[K];
+        if constexpr (CL) {
 #pragma unroll
-        for (int j = 0; j < K; ++j) sl[j] = atomicAdd(&hist[pos[i][j] >> TL], 1u);
+          for (int j = 0; j < K; ++j) sl[j] = atomicAdd(&hcur[pos[i][j] >> TL], 1u);
 #pragma unroll
-        for (int j = 0; j < K; ++j) lpos[sl[j]] = pos[i][j] & tmask;
+          for (int j = 0; j < K; ++j) {
+            if (sl[j] < tcap) lpos[(pos[i][j] >> TL) * tcap + sl[j]] = pos[i][j] & tmask;
+            else ovf = true;
+          }
+        } else {
+#pragma unroll
+          for (int j = 0; j < K; ++j) sl[j] = atomicAdd(&hist[pos[i][j] >> TL], 1u);
+#pragma unroll
+          for (int j = 0; j < K; ++j) lpos[sl[j]] = pos[i][j] & tmask;
+        }
       }
 #ifdef ADL_BLOOM_STAMPS
       if (a.exp & 1) {
@@ -1048,9 +1088,17 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin16_kernel(BuildArgs a, Src key
     const bool last_of_filter = wg + G >= total_chunks || FT::of_chunk(a, ft, wg + G) != fcur;
     uint32_t nv = 0, noff = 0;
     if (CMP && wg + G < total_chunks) nv = rank_live(wg + G, hpar ^ (uint32_t)last_of_filter, noff);
+    if (CL && ovf) oflag[par] = 1u;
     __syncthreads();  // lpos holds chunk c sorted; hist is free; this chunk's marks are in hmask
     STAMP(4);
-    for (uint32_t i = tid; i <= T; i += BLOCK) hist[i] = 0;
+    if constexpr (CL) {
+      // the other counter array and flag were last read before this chunk's
+      // first barrier, and are next used after the next one
+      for (uint32_t i = tid; i < a.hist_words; i += BLOCK) hoth[i] = 0;
+      if (tid == 0) oflag[par ^ 1u] = 0;
+    } else {
+      for (uint32_t i = tid; i <= T; i += BLOCK) hist[i] = 0;
+    }
     if (dd && last_of_filter && wg + G < total_chunks)
       for (uint32_t i = tid; i < (1u << dd); i += BLOCK) dtab[i] = kEmpty;
     if (hot_on && last_of_filter && tid < (int)(kHotN / 32)) {
@@ -1064,7 +1112,64 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin16_kernel(BuildArgs a, Src key
       for (int b = 0; b < 32; ++b)
         *(((mw >> b) & 1u) ? st + b : reinterpret_cast<unsigned long long *>(dummy)) = a.nonce;
     }
-    if constexpr (CMP) {
+    if constexpr (CL) {
+      uint4 *dst = reinterpret_cast<uint4 *>(pos_ws + d.pos_base + (uint64_t)w * a.cap);
+      if (oflag[par] == 0u) {
+        // table entries (start << 16) | count for tiles t < T
+#pragma unroll
+        for (int r = 0; r < TPT; ++r) {
+          const uint32_t t = tid + r * BLOCK;
+          const bool ok = t < T;
+          *(ok ? tab + (uint64_t)t * d.chunks + w : dummy) = ((t * tcap) << 16) | hcur[ok ? t : 0u];
+        }
+        // the region's 16-byte words that hold positions (tile t's slots are
+        // words [t * tcap, t * tcap + count)); v / tq = umulhi(v, mg), exact
+        // for v, tq < 2^16
+        const uint32_t tq = tcap >> 2, nvec = T * tq;
+        const uint32_t mg = 0xffffffffu / tq + 1u;
+#pragma unroll
+        for (int sv = 0; sv < VPT; ++sv) {
+          const uint32_t v = tid + sv * BLOCK;
+          const uint32_t t = __umulhi(v, mg);
+          const bool ok = v < nvec && 4u * (v - t * tq) < hcur[min(t, T - 1u)];
+          *(ok ? dst + v : dummy4) = src4[ok ? v : 0u];
+        }
+      } else {
+        // some tile overflowed its slots: counting-sort this chunk exactly
+        // from the positions still in registers; the entries describe the
+        // dense runs
+        total = block_excl_scan_array<BLOCK>(hcur, T + 1, scratch);
+#pragma unroll
+        for (int r = 0; r < TPT; ++r) {
+          const uint32_t t = tid + r * BLOCK;
+          const bool ok = t < T;
+          const uint32_t s0 = hcur[ok ? t : 0u], s1 = hcur[ok ? t + 1 : 0u];
+          *(ok ? tab + (uint64_t)t * d.chunks + w : dummy) = (s0 << 16) | (s1 - s0);
+        }
+        __syncthreads();  // the starts are read before the cursors move
+#pragma unroll
+        for (int i = 0; i < KPT; ++i) {
+          if ((live >> i) & 1u) {
+            uint32_t sl[K];
+#pragma unroll
+            for (int j = 0; j < K; ++j) sl[j] = atomicAdd(&hcur[pos[i][j] >> TL], 1u);
+#pragma unroll
+            for (int j = 0; j < K; ++j) lpos[sl[j]] = pos[i][j] & tmask;
+          }
+        }
+        __syncthreads();  // the chunk is sorted in lpos
+        const uint32_t tv = total >> 2;
+#pragma unroll
+        for (int sv = 0; sv < VPT; ++sv) {
+          const uint32_t v = tid + sv * BLOCK;
+          const bool ok = v < tv;
+          *(ok ? dst + v : dummy4) = src4[ok ? v : 0u];
+        }
+        const bool ok = (uint32_t)tid < (total & 3u);
+        *(ok ? reinterpret_cast<uint32_t *>(dst) + tv * 4 + tid : dummy) = lpos[ok ? tv * 4 + tid : 0u];
+      }
+      par ^= 1u;
+    } else if constexpr (CMP) {
       hpar ^= (uint32_t)last_of_filter;
       // this chunk's positions out of lpos now, then the next chunk's live keys in
       uint4 *dst = reinterpret_cast<uint4 *>(pos_ws + d.pos_base + (uint64_t)w * a.cap);
@@ -1141,8 +1246,14 @@ __global__ __launch_bounds__(kBlockB, 4 * OCC) void bloom_tile_kernel(BuildArgs 
       const uint32_t i = wb + tid + r * kBlockB;
       rs[r] = re[r] = 0;
       if (i < W) {
-        rs[r] = row0[i];
-        re[r] = row0[i + W];
+        if (a.claim) {  // (start << 16) | length
+          const uint32_t v = row0[i];
+          rs[r] = v >> 16;
+          re[r] = rs[r] + (v & 0xffffu);
+        } else {
+          rs[r] = row0[i];
+          re[r] = row0[i + W];
+        }
       }
     }
   };
@@ -1374,6 +1485,7 @@ struct Plan {
   uint64_t stamp_off = 0;  // byte offset of the collapsed-key stamps (kHotN u64 per filter)
   bool hot = false;        // collapsed keys stamped, not binned (16-byte keys, k = 6; ADL_BLOOM_HOT)
   bool compact = false;    // with hot: pass A compacts the live keys (ADL_BLOOM_COMPACT)
+  bool claim = false;      // claim layout sizes (ADL_BLOOM_CLAIM): bloom_bin16_kernel<..., CL> runs
   uint32_t total_chunks = 0, total_tiles = 0, total_sc = 0;
   uint32_t grid_a = 0, grid_b = 0;  // persistent grids
   uint32_t occ_b = 1;               // pass-B workgroups per CU (ADL_BLOOM_B_OCC)
@@ -1460,18 +1572,61 @@ int make_plan(const uint64_t *counts, uint32_t nf, int32_t bpk, Plan &p) {
     for (uint32_t f = 0; f < nf; ++f) w += (counts[f] + c - 1) / c;
     return w;
   };
-  const uint64_t wmin = nchunks(cmax);
-  uint32_t C;
-  if (wmin >= grid_a_max) {
-    const uint64_t rounds = (wmin + grid_a_max - 1) / grid_a_max;
-    C = (uint32_t)std::min<uint64_t>(
-        cmax, adl_host::round_up((total_n + rounds * grid_a_max - 1) / (rounds * grid_a_max), 4));
-    // the smallest C whose chunks, rounded up per filter, still fill no more rounds
-    while (C + 4 <= cmax && nchunks(C) > rounds * grid_a_max) C += 4;
+  auto pick_c = [&](uint32_t cm) -> uint32_t {
+    const uint64_t wmin = nchunks(cm);
+    uint32_t c;
+    if (wmin >= grid_a_max) {
+      const uint64_t rounds = (wmin + grid_a_max - 1) / grid_a_max;
+      c = (uint32_t)std::min<uint64_t>(
+          cm, adl_host::round_up((total_n + rounds * grid_a_max - 1) / (rounds * grid_a_max), 4));
+      // the smallest C whose chunks, rounded up per filter, still fill no more rounds
+      while (c + 4 <= cm && nchunks(c) > rounds * grid_a_max) c += 4;
+    } else {
+      c = (uint32_t)std::min<uint64_t>(
+          cm, std::max<uint64_t>(256, adl_host::round_up((total_n + grid_a_max - 1) / grid_a_max, 4)));
+    }
+    return c;
+  };
+  // Claim layout (ADL_BLOOM_CLAIM; 16-byte keys and hashed pairs with k = 6,
+  // not with collapsed-key stamping): the region of cap words gives each tile
+  // of a filter cap / T slots.  C shrinks so the region holds k*C positions
+  // times the slack (ADL_BLOOM_CLAIM_SLACK, percent); the layout is kept only
+  // if the largest filter's share per tile clears its mean run by
+  // ADL_BLOOM_CLAIM_SIGMA standard deviations (Poisson), so overflowing chunks
+  // (sorted exactly, more slowly) stay rare.  The region takes all the LDS
+  // left over (fewer overflows); ADL_BLOOM_CLAIM_CAP (percent of k*C) caps it
+  // and ADL_BLOOM_CLAIM=2 skips the share test: the tests force overflowing
+  // chunks that way.  Default (unset): only filters of at most kClaimTiles
+  // tiles, the one shape class where it measured faster (256 x 10 K keys:
+  // pass A + B 92 against 109 us; 32 x 100 K equal; 256 x 40 K and 64 x 300 K
+  // 4-11 % slower; profiles/r04/ab_claim_shapes.log).
+  const uint32_t claim_mode = env_u32("ADL_BLOOM_CLAIM", 3);
+  bool claim = k == 6 && env_flag("ADL_BLOOM_HOT", 0) == 0 && claim_mode != 0;
+  const int64_t room_cl = (int64_t)lds_words_a - 2 * hist_words - 36 - 256;  // region + C
+  uint32_t cap_cl = 0;
+  uint32_t C = 0;
+  if (claim && room_cl > 64) {
+    const uint32_t slack = std::max<uint32_t>(env_u32("ADL_BLOOM_CLAIM_SLACK", 125), 100);
+    const uint32_t cm = std::min<uint32_t>(block_a * kpt, (uint32_t)(room_cl * 100 / (slack * k + 100))) & ~3u;
+    if (cm >= 4) {
+      C = pick_c(cm);
+      int64_t cw = std::min<int64_t>(room_cl - C, 36ll * block_a);  // <= 4 * VPT * BLOCK
+      if (const uint32_t pct = env_u32("ADL_BLOOM_CLAIM_CAP", 0))
+        cw = std::min<int64_t>(cw, (int64_t)k * C * std::max<uint32_t>(pct, 100) / 100 + 3);
+      cap_cl = (uint32_t)cw & ~3u;
+      const uint32_t tmax = (uint32_t)tiles_at(TL, true);
+      const uint32_t tcap = (cap_cl / tmax) & ~3u;
+      const double mu = (double)k * C / tmax;
+      const double sig = env_u32("ADL_BLOOM_CLAIM_SIGMA", 4);
+      claim = cap_cl >= k * C && tcap >= 16 && (claim_mode == 2 || tcap >= mu + sig * std::sqrt(mu) + 8) &&
+              (claim_mode != 3 || tmax <= kClaimTiles);
+    } else {
+      claim = false;
+    }
   } else {
-    C = (uint32_t)std::min<uint64_t>(
-        cmax, std::max<uint64_t>(256, adl_host::round_up((total_n + grid_a_max - 1) / grid_a_max, 4)));
+    claim = false;
   }
+  if (!claim) C = pick_c(cmax);
   p.a.nf = nf;
   p.a.xcd_remap = env_flag("ADL_BLOOM_XCD_REMAP", 1);
   p.a.nt_keys = env_flag("ADL_BLOOM_NT_KEYS", 1);
@@ -1507,8 +1662,9 @@ int make_plan(const uint64_t *counts, uint32_t nf, int32_t bpk, Plan &p) {
   p.a.k = k;
   p.a.C = C;
   p.a.TL = TL;
-  const uint32_t cap = k * C;
+  const uint32_t cap = claim ? cap_cl : k * C;
   p.a.cap = cap;
+  p.claim = claim;
   p.a.hist_words = hist_words;
   uint64_t pos = 0, tab = 0, boff = 0;
   uint32_t chunk = 0, tile = 0, sc = 0;
@@ -1553,7 +1709,7 @@ int make_plan(const uint64_t *counts, uint32_t nf, int32_t bpk, Plan &p) {
   p.ft_bytes = p.dt ? adl_host::round_up(nf * sizeof(FilterDesc), 256) + 4ull * (chunk + tile + sc) + 256 : 0;
   p.stamp_off = adl_host::round_up((p.pos_words + p.table_words + p.scratch_words + p.hash_words) * 4 + p.ft_bytes, 256);
   p.ws_bytes = p.stamp_off + (uint64_t)nf * kHotN * 8 + 256;
-  p.lds_a = (size_t)(hist_words + 32 + (k + 1) * C + 256) * 4;
+  p.lds_a = claim ? (size_t)(2 * hist_words + 36 + cap + C + 256) * 4 : (size_t)(hist_words + 32 + (k + 1) * C + 256) * 4;
   p.lds_b = (size_t)((1u << (TL - 5)) + 2 * kSegBatch + 4) * 4;
   p.grid_a = std::min<uint32_t>(p.total_chunks, grid_a_max);
   p.block_a = block_a;
@@ -1579,8 +1735,10 @@ int make_plan(const uint64_t *counts, uint32_t nf, int32_t bpk, Plan &p) {
   }
   p.grid_b = std::min<uint32_t>(p.total_tiles, p.occ_b * cus);
   if (adl_host::env_on("ADL_BLOOM_DEBUG", false))
-    fprintf(stderr, "adl_bloom plan: filters %u, tile 2^%u bits, tiles %u, C %u, chunks %u, pass B %u per CU, depth %u\n",
-            nf, TL, p.total_tiles, C, p.total_chunks, p.occ_b, p.depth);
+    fprintf(stderr,
+            "adl_bloom plan: filters %u, tile 2^%u bits, tiles %u, C %u, chunks %u, region %u words%s, pass B %u per CU, "
+            "depth %u\n",
+            nf, TL, p.total_tiles, C, p.total_chunks, cap, claim ? " (claim)" : "", p.occ_b, p.depth);
   return ADL_OK;
 }
 
@@ -1627,6 +1785,10 @@ uint64_t next_nonce() {
   return v;
 }
 
+// pass A of this thread's last launch pair wrote the claim layout's table
+// (adl_bloom_build_positions reads it)
+thread_local bool t_last_claim = false;
+
 template <bool DT, class Keys>
 int launch_binned_dt(const Plan &p, Keys keys, uint8_t *d_bitmaps, void *ws, hipStream_t st) {
   BuildArgs aa = p.a;
@@ -1634,7 +1796,9 @@ int launch_binned_dt(const Plan &p, Keys keys, uint8_t *d_bitmaps, void *ws, hip
   aa.nonce = next_nonce();
   aa.hot = 0;
   aa.compact = 0;
+  aa.claim = 0;
   uint32_t hot_used = 0;  // pass A stamped collapsed keys: pass B adds their bits
+  uint32_t claim_used = 0;  // pass A wrote the claim layout's table entries
   uint32_t *pos_ws = reinterpret_cast<uint32_t *>(ws);
   uint32_t *tab_ws = pos_ws + p.pos_words;
   uint32_t *queue = tab_ws + p.table_words;  // pass B tile queue, then pass A's scratch lines
@@ -1682,6 +1846,11 @@ int launch_binned_dt(const Plan &p, Keys keys, uint8_t *d_bitmaps, void *ws, hip
             return go_src(adl_host::lds_limit<bloom_bin16_kernel<B, 6, Src16, DT, true>>,
                           bloom_bin16_kernel<B, 6, Src16, DT, true>, ah, Src16{keys.keys}, false);
           }
+          if (p.claim) {
+            ah.claim = claim_used = 1;
+            return go_src(adl_host::lds_limit<bloom_bin16_kernel<B, 6, Src16, DT, false, true>>,
+                          bloom_bin16_kernel<B, 6, Src16, DT, false, true>, ah, Src16{keys.keys}, false);
+          }
           return go_src(adl_host::lds_limit<bloom_bin16_kernel<B, 6, Src16, DT>>, bloom_bin16_kernel<B, 6, Src16, DT>,
                         ah, Src16{keys.keys}, false);
         }
@@ -1713,6 +1882,11 @@ int launch_binned_dt(const Plan &p, Keys keys, uint8_t *d_bitmaps, void *ws, hip
           // pass B 64 -> 70 us with it)
           BuildArgs av = aa;
           av.dd_log2 = 0;
+          if (p.claim) {
+            av.claim = claim_used = 1;
+            return go_src(adl_host::lds_limit<bloom_bin16_kernel<B, 6, SrcH, DT, false, true>>,
+                          bloom_bin16_kernel<B, 6, SrcH, DT, false, true>, av, SrcH{hp, p.a.C}, true);
+          }
           return go_src(adl_host::lds_limit<bloom_bin16_kernel<B, 6, SrcH, DT>>, bloom_bin16_kernel<B, 6, SrcH, DT>,
                         av, SrcH{hp, p.a.C}, true);
         }
@@ -1729,6 +1903,8 @@ int launch_binned_dt(const Plan &p, Keys keys, uint8_t *d_bitmaps, void *ws, hip
   }
   BuildArgs ab = aa;
   ab.hot = hot_used;
+  ab.claim = claim_used;
+  t_last_claim = claim_used != 0;
   if (!p.total_chunks) ab.dyn_tiles = 0;  // no pass A ran to reset the queue
   auto go_b = [&](auto lim, auto kern) -> int {
     if (int rc = lim()) return rc;
@@ -2079,6 +2255,14 @@ int adl_bloom_build_positions(const uint64_t *key_counts, uint32_t num_filters, 
     uint64_t sum = 0;
     std::vector<uint32_t> row;
     for (const FilterDesc &d : p.f) {  // row T of each filter's table: every chunk's total
+      if (t_last_claim) {  // claim layout: the lengths in rows 0..T-1
+        row.resize((uint64_t)d.tiles * d.chunks);
+        if (row.empty()) continue;
+        ADL_HIP_TRY(hipMemcpyAsync(row.data(), tab + d.table_base, row.size() * 4ull, hipMemcpyDeviceToHost, st));
+        ADL_HIP_TRY(hipStreamSynchronize(st));
+        for (uint32_t v : row) sum += v & 0xffffu;
+        continue;
+      }
       row.resize(d.chunks);
       if (!d.chunks) continue;
       ADL_HIP_TRY(hipMemcpyAsync(row.data(), tab + d.table_base + (uint64_t)d.tiles * d.chunks, d.chunks * 4ull,
