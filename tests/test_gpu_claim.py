@@ -149,3 +149,21 @@ def test_claim_segmented_varlen_many_filters(dev, ab, oracle, claim):
     for f in range(len(sizes)):
         want = oracle.keys2block(keys[int(kb[f]):int(kb[f + 1])])
         assert np.array_equal(out[int(boff[f]):int(boff[f]) + int(nbytes[f])], want), f
+
+
+def test_claim_positions_count(dev, ab, oracle, claim, monkeypatch):
+    """adl_bloom_build_positions reads the claim layout's (start, length)
+    entries: with the pair table off every key writes k = 6 positions, and
+    the bitmaps still equal the oracle's (256 filters of 10 K keys, the
+    default's claim shape)."""
+    monkeypatch.setenv("ADL_BLOOM_HASH_DEDUP", "0")
+    sizes = [10_000] * 255 + [9_999]
+    kb = np.concatenate([[0], np.cumsum(sizes)]).astype(np.uint64)
+    keys = ab.synth_keys16(int(kb[-1]), seed=99)
+    sb = ab.SegmentedBuilder(kb)
+    out = sb.build(keys).cpu().numpy()
+    assert sb.positions() == 6 * int(kb[-1])
+    hk = keys.cpu().numpy()
+    for f in (0, 1, 128, 255):
+        o = int(sb.boff[f])
+        assert np.array_equal(out[o:o + int(sb.sizes[f])], oracle.keys2block(hk[kb[f]:kb[f + 1]])), f
