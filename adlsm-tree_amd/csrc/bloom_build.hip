@@ -65,7 +65,7 @@ constexpr uint32_t kFewTiles = 256;       // tiles per filter below which smalle
 constexpr uint32_t kMinRun = 64;          // ... while a chunk's run per tile stays this long (positions)
 constexpr uint32_t kChunkEst = 5500;      // keys per pass-A chunk (k = 6), for that estimate
 constexpr uint32_t kHotN = 4096;          // collapsed-key indices per filter (hash16h)
-constexpr uint32_t kClaimTiles = 8;       // claim layout by default only up to this many tiles per filter
+constexpr uint32_t kClaimTiles = 10;      // claim layout by default only up to this many tiles per filter
 
 struct FilterDesc {
   uint64_t key_begin;   // first key (index into the key set)
@@ -1597,9 +1597,10 @@ int make_plan(const uint64_t *counts, uint32_t nf, int32_t bpk, Plan &p) {
   // left over (fewer overflows); ADL_BLOOM_CLAIM_CAP (percent of k*C) caps it
   // and ADL_BLOOM_CLAIM=2 skips the share test: the tests force overflowing
   // chunks that way.  Default (unset): only filters of at most kClaimTiles
-  // tiles, the one shape class where it measured faster (256 x 10 K keys:
-  // pass A + B 92 against 109 us; 32 x 100 K equal; 256 x 40 K and 64 x 300 K
-  // 4-11 % slower; profiles/r04/ab_claim_shapes.log).
+  // tiles, where it measured faster (pass A + B: 512 x 5 K keys 119 against
+  // 164 us, 256 x 10 K 92 / 109, 256 x 20 K 124 / 143, 128 x 30 K 94 / 101;
+  // 128 x 60 K and 32 x 100 K equal; 256 x 40 K and 64 x 300 K 4-11 % slower;
+  // profiles/r04/ab_claim_shapes.log, ab_claim_threshold.log).
   const uint32_t claim_mode = env_u32("ADL_BLOOM_CLAIM", 3);
   bool claim = k == 6 && env_flag("ADL_BLOOM_HOT", 0) == 0 && claim_mode != 0;
   const int64_t room_cl = (int64_t)lds_words_a - 2 * hist_words - 36 - 256;  // region + C

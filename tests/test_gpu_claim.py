@@ -61,7 +61,7 @@ def test_claim_plan_selected(dev, ab, monkeypatch, capfd):
     assert "(claim)" in capfd.readouterr().err
     assert ab.workspace_bytes([10_000_000], 10) > 0
     assert "(claim)" not in capfd.readouterr().err
-    # default: only filters of at most 8 tiles (256 x 10 K: 4 tiles each)
+    # default: only filters of at most 10 tiles (256 x 10 K: 4 tiles each)
     monkeypatch.delenv("ADL_BLOOM_CLAIM")
     assert ab.workspace_bytes([10_000] * 256, 10) > 0
     assert "(claim)" in capfd.readouterr().err

@@ -27,6 +27,9 @@ def run(keys, kb, reps):
 SHAPES = [("256 x 10K", [10_000] * 256, "1"), ("32 x 100K", [100_000] * 32, "1"),
           ("256 x 40K", [40_000] * 256, "1"), ("64 x 300K", [300_000] * 64, "1"),
           ("8 x 1M (forced)", [1_000_000] * 8, "2"), ("1 x 10M (forced)", [10_000_000], "2")]
+if len(sys.argv) > 1 and sys.argv[1] == "threshold":  # around the default's 8-tile limit
+    SHAPES = [("512 x 5K", [5_000] * 512, "1"), ("256 x 20K", [20_000] * 256, "1"),
+              ("128 x 30K", [30_000] * 128, "1"), ("128 x 60K", [60_000] * 128, "1")]
 for name, counts, mode in SHAPES:
     keys = torch.cat([ab.synth_keys16(c, seed=0x5EED + i) for i, c in enumerate(counts)])
     kb = np.concatenate([[0], np.cumsum(counts)]).astype(np.uint64)
