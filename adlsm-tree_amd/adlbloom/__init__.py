@@ -46,6 +46,7 @@ EXPORTS = (
     "adl_bloom_profile_enable", "adl_bloom_profile_collect", "adl_synth_probe_queries_device",
     "adl_bloom_profile_each", "adl_bloom_probe_batch_workspace_bytes", "adl_bloom_probe_batch_device",
     "adl_bloom_test_fault", "adl_bloom_build_positions", "adl_bloom_get_device", "adl_bloom_set_device",
+    "adl_bloom_reload_knobs", "adl_bloom_build_segmented_ex", "adl_bloom_probe_server_launches",
 )
 
 _LIB = None
@@ -78,6 +79,7 @@ def lib() -> ctypes.CDLL:
         "adl_bloom_build_segmented_device": (ctypes.c_int, [vp, vp, u32, vp, u32, i32, vp, vp, vp, u64, vp]),
         "adl_bloom_build": (ctypes.c_int, [vp, vp, u64, u32, i32, vp, vp]),
         "adl_bloom_build_segmented": (ctypes.c_int, [vp, vp, u32, vp, u32, i32, vp, vp, vp]),
+        "adl_bloom_build_segmented_ex": (ctypes.c_int, [vp, vp, u32, vp, u32, i32, vp, vp, u32, vp]),
         "adl_bloom_filter_block_bytes": (u64, [vp, u32, i32]),
         "adl_bloom_filter_block_workspace_bytes": (u64, [vp, u32, i32]),
         "adl_bloom_filter_block_build_device": (ctypes.c_int, [vp, vp, u32, vp, u32, i32, vp, u64, vp, u64, vp]),
@@ -114,6 +116,7 @@ def lib() -> ctypes.CDLL:
         "adl_bloom_build_positions": (ctypes.c_int, [vp, u32, i32, vp, ctypes.POINTER(u64), vp]),
         "adl_bloom_get_device": (ctypes.c_int, [ctypes.POINTER(i32)]),
         "adl_bloom_set_device": (ctypes.c_int, [i32]),
+        "adl_bloom_reload_knobs": (ctypes.c_int, []),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -121,6 +124,12 @@ def lib() -> ctypes.CDLL:
         fn.argtypes = args
     _LIB = L
     return L
+
+
+def reload_knobs() -> None:
+    """Re-read the ADL_BLOOM_* switches (the library reads them once per
+    process; tests that change them call this, with no call running)."""
+    _check(lib().adl_bloom_reload_knobs(), "adl_bloom_reload_knobs")
 
 
 def _check(status: int, what: str) -> None:
@@ -315,17 +324,22 @@ def _host_ptr(a):
     return a.data_ptr()
 
 
-def build_segmented_host(keys, key_begin, out, bitmap_off, offsets=None, bits_per_key: int = 10, stream=None):
-    """Host-pointer pipelined segmented build (adl_bloom_build_segmented):
-    keys (n, stride) uint8 or packed bytes + offsets (n+1) in host memory
-    (numpy, or CPU torch tensors -- pinned ones are DMAed directly); filter f's
-    exact-length bitmap lands at out[bitmap_off[f]:] (out: host uint8 buffer)."""
+def build_segmented_host(keys, key_begin, out, bitmap_off, offsets=None, bits_per_key: int = 10, stream=None,
+                         flags: int = 0):
+    """Host-pointer pipelined segmented build (adl_bloom_build_segmented, or
+    _ex with flags): keys (n, stride) uint8 or packed bytes + offsets (n+1) in
+    host memory (numpy, or CPU torch tensors -- pinned ones are DMAed
+    directly); filter f's exact-length bitmap lands at out[bitmap_off[f]:]
+    (out: host uint8 buffer)."""
     kb = np.ascontiguousarray(key_begin, dtype=np.uint64)
     bo = np.ascontiguousarray(bitmap_off, dtype=np.uint64)
     stride = 0 if offsets is not None else int(keys.shape[1])
-    _check(lib().adl_bloom_build_segmented(_host_ptr(keys), None if offsets is None else _host_ptr(offsets),
-                                           stride, kb.ctypes.data, len(kb) - 1, bits_per_key, _host_ptr(out),
-                                           bo.ctypes.data, _stream(stream)), "adl_bloom_build_segmented")
+    args = (_host_ptr(keys), None if offsets is None else _host_ptr(offsets), stride, kb.ctypes.data, len(kb) - 1,
+            bits_per_key, _host_ptr(out), bo.ctypes.data)
+    if flags:
+        _check(lib().adl_bloom_build_segmented_ex(*args, flags, _stream(stream)), "adl_bloom_build_segmented_ex")
+    else:
+        _check(lib().adl_bloom_build_segmented(*args, _stream(stream)), "adl_bloom_build_segmented")
     return out
 
 

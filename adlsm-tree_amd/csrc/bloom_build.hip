@@ -26,8 +26,10 @@
 // Variable-length keys are hashed first, in length-sorted runs staged in LDS
 // (hash_var_kernel), and pass A then bins the (h1, h2) pairs.
 //
-// A direct device-scope atomicOr kernel (bloom_atomic_kernel) is kept as the
-// alternative for small filters and as an independent cross-check.
+// Designs measured slower (a direct atomicOr build, collapsed-key stamping,
+// live-key compaction, a bucketed pass A, split-seed hashing, dynamic tile
+// queues, ...) are not in this library; DESIGN.md §5 keeps their numbers and
+// git history their code.
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -36,15 +38,13 @@
 
 #include <algorithm>
 #include <atomic>
-#include <chrono>
 #include <cmath>
-#include <random>
 #include <mutex>
 #include <type_traits>
 #include <vector>
 
-#include "bloom_bucket.hpp"
 #include "bloom_common.hpp"
+#include "probe_server.hpp"
 
 using namespace adl_dev;
 
@@ -64,8 +64,17 @@ constexpr uint32_t kTargetWorkgroups = 512;
 constexpr uint32_t kFewTiles = 256;       // tiles per filter below which smaller tiles are taken
 constexpr uint32_t kMinRun = 64;          // ... while a chunk's run per tile stays this long (positions)
 constexpr uint32_t kChunkEst = 5500;      // keys per pass-A chunk (k = 6), for that estimate
-constexpr uint32_t kHotN = 4096;          // collapsed-key indices per filter (hash16h)
 constexpr uint32_t kClaimTiles = 10;      // claim layout by default only up to this many tiles per filter
+constexpr uint32_t kClaimSlack = 125;     // claim layout: region = k*C positions * 125 %
+constexpr uint32_t kClaimSigma = 4;       // ... kept when a tile's share clears its mean run by 4 sigma
+constexpr uint32_t kHvKeys = 512;         // keys per hash_var_kernel run
+constexpr uint32_t kBlockA = 1024;        // pass A threads per workgroup (one workgroup per CU)
+constexpr uint32_t kDdLog2Max = 11;       // log2 slots of pass A's repeated-hash table, at most
+// LDS pass A leaves free on its CU (3 KiB): the resident probe server's
+// workgroup (probe_server.hip, 2 KiB) fits beside it, so a Get never waits for
+// a build's persistent grid (DB::Get probes while DoCompaction builds,
+// src/db.cpp:164-172, 263).  The headline's chunk still fits 7 whole rounds.
+constexpr uint32_t kLdsReserveWords = 768;
 
 struct FilterDesc {
   uint64_t key_begin;   // first key (index into the key set)
@@ -90,39 +99,19 @@ struct BuildArgs {
   uint32_t TL;     // log2 tile bits
   uint32_t cap;    // positions per chunk region (k*C; C % 4 == 0 keeps regions 16-byte aligned)
   uint32_t hist_words;  // pass A LDS tile counters (max tiles per filter + 1, rounded to 4)
-  uint32_t xcd_remap;  // consecutive chunks / tiles on one XCD (tuning, ADL_BLOOM_XCD_REMAP)
-  uint32_t nt_keys;    // pass A: non-temporal key loads (tuning, ADL_BLOOM_NT_KEYS)
-  uint32_t nt_bitmap;  // pass B: non-temporal bitmap stores (tuning, ADL_BLOOM_NT_BITMAP)
-  uint32_t dyn_tiles;  // pass B: tiles from a work queue that pass A resets (ADL_BLOOM_DYN_TILES)
-  uint32_t stage_keys; // pass A: LDS-staged variable-length keys (16-B aligned key buffer; ADL_BLOOM_STAGE_KEYS)
+  uint32_t stage_keys; // pass A: LDS-staged variable-length keys (16-byte-aligned key buffers only)
   uint32_t dedup;      // skip a key equal to its predecessor in the same filter (ADL_BLOOM_SKIP_ADJACENT_DUPLICATES)
-  uint32_t scan1;      // pass A: one-barrier tile-count scan (ADL_BLOOM_SCAN1)
-  uint32_t hv_keys;    // keys per hash_var_kernel run (ADL_BLOOM_HV_KEYS)
-  uint32_t hv_split;   // hash_var_kernel: a run's longest groups hashed by two waves, one seed each (ADL_BLOOM_HV_SPLIT)
-  // Claim layout (ADL_BLOOM_CLAIM; bloom_bin16_kernel<..., CL> and the pass B
-  // after it): a chunk region gives each of a filter's T tiles tcap = (cap / T)
-  // & ~3 fixed slots, a position takes its slot with one ds_add_rtn (no count
-  // pass, no scan), and a (tile, chunk) table entry is (start << 16) | length.
+  // Claim layout (bloom_bin16_kernel<..., CL> and the pass B after it): a chunk
+  // region gives each of a filter's T tiles tcap = (cap / T) & ~3 fixed slots,
+  // a position takes its slot with one ds_add_rtn (no count pass, no scan), and
+  // a (tile, chunk) table entry is (start << 16) | length.
   uint32_t claim;
-  uint32_t dd_log2;   // bloom_bin16_kernel: log2 slots of the (h1, h2) table that skips repeated hashes
+  uint32_t dd_log2;    // bloom_bin16_kernel: log2 slots of the table that skips repeated hashes
                        // (0: off; ADL_BLOOM_HASH_DEDUP)
-  uint32_t dd_mode;    // 1: every key claims its (h1, h2); 2: keys with h1 == h2 claim h1 (ADL_BLOOM_DD_MODE)
-  uint32_t var_hash;   // variable-length keys: length-sorted hashing pass + pass A over (h1, h2) (ADL_BLOOM_VAR_HASH)
   uint32_t exp;        // diagnostics build only (ADL_BLOOM_EXP bits, wrong results): pass A 1 no hash,
-                       // 2 no position stores, 32 no reduction; pass B 4 no ds_or, 8 no bitmap stores
-  // Collapsed 16-byte keys (hash16h, ADL_BLOOM_HOT): pass A stamps each present
-  // index i of a filter (stamps[f*kHotN + i] = nonce, a value unique to this
-  // launch pair) instead of binning the key's k positions; pass B ORs
-  // (j+1)*hot_h16(i) % m for the stamped indices into its tiles.  Set by the
-  // host per launch: pass A's flag only for bloom_bin16_kernel over 16-byte keys.
-  uint32_t hot;
-  // Live-key compaction (with hot; ADL_BLOOM_COMPACT): the keys of a chunk that
-  // still bin positions (valid, not collapsed) are ranked across the workgroup
-  // and their (h1, h2) staged densely in LDS, so the count and scatter run over
-  // ceil(live / BLOCK) key slots.
-  uint32_t compact;
-  uint64_t nonce;
-  uint64_t *stamps;
+                       // 2 no position stores, 32 no reduction; pass B 4 no ds_or, 8 no bitmap stores;
+                       // hashing pass 16 no hashing
+  uint32_t pad_;
   FilterDesc f[kMaxFilters];
 };
 
@@ -197,15 +186,46 @@ struct Filt<true> {  // descriptors in the workspace's FilterTable
 
 // FilterTable maps: block f writes filter f's chunk, tile and run ranges.
 __global__ __launch_bounds__(256) void fill_maps_kernel(const FilterDesc *__restrict__ fd, uint32_t *__restrict__ chunk_f,
-                                                        uint32_t *__restrict__ tile_f, uint32_t *__restrict__ sc_f,
-                                                        uint32_t hv_keys) {
+                                                        uint32_t *__restrict__ tile_f, uint32_t *__restrict__ sc_f) {
   const uint32_t f = blockIdx.x;
   const FilterDesc d = fd[f];
   for (uint32_t i = threadIdx.x; i < d.chunks; i += 256) chunk_f[d.chunk_base + i] = f;
   for (uint32_t i = threadIdx.x; i < d.tiles; i += 256) tile_f[d.tile_base + i] = f;
-  const uint32_t runs = (d.n + hv_keys - 1) / hv_keys;
+  const uint32_t runs = (d.n + kHvKeys - 1) / kHvKeys;
   for (uint32_t i = threadIdx.x; i < runs; i += 256) sc_f[d.sc_base + i] = f;
 }
+
+// ---------------------------------------------------------------- work queues
+// A persistent grid's static order assigns workgroup b the items of stripe b,
+// so a workgroup that starts late or runs slow -- one sharing its CU with the
+// resident probe server's wave (probe_server.hip) -- makes the whole pass
+// wait for its stripe.  While a server exists the build passes take their
+// items from these queues instead: XCD group h = blockIdx % 8 (workgroups
+// that share an L2) hands out the items of the static order's group h (item
+// i of round r is r*G + h*(G/8) + i % (G/8)) through counter q[16h], and a
+// workgroup whose group has run dry takes from the next groups.  A slow
+// workgroup then just takes fewer items.  The counters start at 0 (the host
+// clears them before pass A).  Called by one thread; G % 8 == 0.
+constexpr uint32_t kQueueWords = 256;  // pass A's 8 counters, then pass B's, 64 B apart
+struct GroupQueue {
+  uint32_t *q;
+  uint32_t G, total, g;
+  uint32_t dry;  // bit h: group h ran dry (this thread's view)
+  __device__ GroupQueue(uint32_t *q_, uint32_t G_, uint32_t total_)
+      : q(q_), G(G_), total(total_), g(blockIdx.x % 8), dry(0) {}
+  __device__ uint32_t next() {
+    const uint32_t per = G / 8;
+    for (uint32_t s = 0; s < 8; ++s) {
+      const uint32_t h = (g + s) & 7u;
+      if ((dry >> h) & 1u) continue;
+      const uint32_t i = atomicAdd(q + 16 * h, 1u);
+      const uint32_t t = (i / per) * G + h * per + i % per;
+      if (t < total) return t;
+      dry |= 1u << h;
+    }
+    return total;
+  }
+};
 
 // ---------------------------------------------------------------- diagnostics
 // Built only with -DADL_BLOOM_STAMPS (make stamps): wave 0 of every
@@ -235,6 +255,11 @@ __device__ uint64_t g_stamps[3][2048][8];  // pass A, pass B, hashing pass
 #endif
 
 // ---------------------------------------------------------------- pass A
+// At most 120 VGPRs per lane (the attribute counts arch VGPRs and is doubled
+// for gfx950's unified file): four pass-A waves per SIMD then leave 32, the
+// resident probe server's wave (probe_server.hip), so a Get is served on the
+// same CU while a build runs.
+#define kPassARegs __attribute__((amdgpu_num_vgpr(60)))
 // Register prefetch of a chunk's keys.  Only the fixed 16-byte view has raw
 // words worth holding (4 VGPRs per key); the other views hash straight from
 // memory.
@@ -249,23 +274,21 @@ struct KeyRegs<Keys16> {
   uint4 raw;
 };
 
-// Persistent, two workgroups per CU (<= 80 KiB LDS each) so one workgroup's
-// hashing overlaps the other's LDS sort and stores.  A workgroup processes
-// one chunk per round of the grid; the keys of its next chunk are already in
-// flight into registers while the current one is hashed, sorted and stored.
+// The generic pass A (any key shape, any k, adjacent-duplicate skipping).
+// Persistent, one workgroup per CU.  A workgroup processes one chunk per round
+// of the grid; the keys of its next chunk are already in flight into
+// registers while the current one is hashed, sorted and stored.
 //
 // KFIX > 0: k known at compile time, positions kept in registers between the
 // count and the scatter; KFIX == 0: runtime k, positions recomputed.
 template <int BLOCK, int KFIX, int KPT, class Keys, bool DT>
-__global__ __launch_bounds__(BLOCK) void bloom_bin_kernel(BuildArgs a, Keys keys,
+__global__ __launch_bounds__(BLOCK) kPassARegs void bloom_bin_kernel(BuildArgs a, Keys keys,
                                                             uint32_t *__restrict__ pos_ws,
                                                             uint32_t *__restrict__ table_ws,
-                                                            uint32_t total_chunks, uint32_t *__restrict__ tile_queue,
-                                                            FilterTable ft) {
+                                                            uint32_t total_chunks, FilterTable ft) {
   using FT = Filt<DT>;
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   const int tid = threadIdx.x;
-  if (blockIdx.x == 0 && tid == 0) *tile_queue = 0;  // pass B's tile queue
   const uint32_t C = a.C;
   const uint32_t k = KFIX > 0 ? (uint32_t)KFIX : a.k;
   const uint32_t TL = a.TL;
@@ -293,8 +316,7 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin_kernel(BuildArgs a, Keys keys
       for (int i = 0; i < KPT; ++i) {
         const uint32_t idx = tid + i * BLOCK;
         if (idx < cnt) {
-          const uint4 *src = keys.keys + d.key_begin + first + idx;
-          r[i].raw = a.nt_keys ? load_nt(src) : *src;
+          r[i].raw = load_nt(keys.keys + d.key_begin + first + idx);
         }
       }
     }
@@ -306,8 +328,7 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin_kernel(BuildArgs a, Keys keys
   // table entries of neighbouring chunks -- one 64-byte line holds 16 -- are
   // written from one L2.  Speed only: any placement gives the same result.
   const uint32_t G = gridDim.x;
-  const uint32_t slot =
-      (a.xcd_remap && G % 8 == 0) ? (blockIdx.x % 8) * (G / 8) + blockIdx.x / 8 : blockIdx.x;
+  const uint32_t slot = G % 8 == 0 ? (blockIdx.x % 8) * (G / 8) + blockIdx.x / 8 : blockIdx.x;
   const uint32_t rounds = (total_chunks + G - 1) / G;
   KeyRegs<Keys> cur[KPT];
   if (slot < total_chunks) fetch(slot, cur);
@@ -492,8 +513,7 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin_kernel(BuildArgs a, Keys keys
 
     // Exclusive scan: hist[t] = start of tile t's run; hist[T] = k * live keys.
     // the table rows below are written by the thread that scanned them
-    const uint32_t total = a.scan1 ? block_excl_scan_array_1b<BLOCK>(hist, T + 1, scratch)
-                                   : block_excl_scan_array<BLOCK>(hist, T + 1, scratch);
+    const uint32_t total = block_excl_scan_array_1b<BLOCK>(hist, T + 1, scratch);
 
     // (tile, chunk) table, T+1 rows of W entries: row t = start of tile t.
     uint32_t *tab = table_ws + d.table_base;
@@ -677,38 +697,10 @@ __global__ __launch_bounds__(kHvBlock) void hash_var_kernel(BuildArgs a, KeysVar
   // longest groups first (slots are sorted by length): the waves start on the
   // groups that set the workgroup's end, and the short ones fill in behind.
   // (A queue handing each free wave the next group measured the same: the
-  // longest group alone sets the end.)
-  // The `sp` longest groups first, each split between two waves by seed
-  // (waves 2q and 2q+1 take group groups-1-q): their keys set the workgroup's
-  // end, and one seed's chain is about three quarters of both seeds' work.
-  // The other groups follow, longest first, starting with the waves that
-  // split the shorter of them.
-  const uint32_t sp = min(min(a.hv_split, NW / 2), groups);
-  if (wave < 2 * sp) {
-    const uint32_t g = groups - 1 - wave / 2, sd = wave & 1u;
-    const uint32_t s = g * kWave + lane;
-    if (s < cnt) {
-      uint32_t len = s_len[s];
-      const uint32_t r = s_rel[s];
-      uint32_t h;
-      if (len < 0xffffu && (uint64_t)r + len <= sbytes) {
-        h = hash_lds1(stage, r, len, sd ? kSeed2 : kSeed1);
-      } else {
-        uint64_t k0 = base16 + r;
-        if (len == 0xffffu) {
-          k0 = keys.offs[kb + r];
-          len = (uint32_t)(keys.offs[kb + r + 1] - k0);
-        }
-        uint32_t h1, h2;
-        hash_bytes(keys.keys + k0, len, kSeed1, kSeed2, h1, h2);
-        h = sd ? h2 : h1;
-      }
-      reinterpret_cast<uint32_t *>(out + s)[sd] = h;
-    }
-  }
-  const uint32_t rot = (wave + NW - 2 * sp) % NW;  // waves past the split ones start phase 2
-  for (uint32_t gi = rot; gi + sp < groups; gi += NW) {
-    const uint32_t g = groups - 1 - sp - gi;
+  // longest group alone sets the end; so did splitting the longest groups
+  // between two waves by seed, which was slower.)
+  for (uint32_t gi = wave; gi < groups; gi += NW) {
+    const uint32_t g = groups - 1 - gi;
     const uint32_t s = g * kWave + lane;
     if (s >= cnt) continue;
     uint32_t len = s_len[s];
@@ -745,10 +737,6 @@ struct Src16 {
     return load_nt(keys + d.key_begin + first + idx);
   }
   __device__ static __forceinline__ void hash(const Raw &r, uint32_t &h1, uint32_t &h2) { hash16(r, h1, h2); }
-  // hot: collapsed key, h1 = its index (hash16h)
-  __device__ static __forceinline__ void hash_hot(const Raw &r, uint32_t &h1, uint32_t &h2, bool &hot, bool en) {
-    hash16h(r, h1, h2, hot, en);
-  }
 };
 
 typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
@@ -763,10 +751,6 @@ struct SrcH {
   __device__ static __forceinline__ void hash(const Raw &r, uint32_t &h1, uint32_t &h2) {
     h1 = r.x;
     h2 = r.y;
-  }
-  __device__ static __forceinline__ void hash_hot(const Raw &r, uint32_t &h1, uint32_t &h2, bool &hot, bool) {
-    hash(r, h1, h2);
-    hot = false;
   }
 };
 
@@ -787,20 +771,18 @@ struct SrcH {
 // share (rare: the share is the mean plus several standard deviations) is
 // counting-sorted exactly as above from the positions still in registers,
 // and its table entries describe the dense runs instead.
-template <int BLOCK, int K, class Src, bool DT, bool CMP = false, bool CL = false>
-__global__ __launch_bounds__(BLOCK) void bloom_bin16_kernel(BuildArgs a, Src keys,
+template <int BLOCK, int K, class Src, bool DT, bool CL = false, bool DYN = false>
+__global__ __launch_bounds__(BLOCK) kPassARegs void bloom_bin16_kernel(BuildArgs a, Src keys,
                                                               uint32_t *__restrict__ pos_ws,
                                                               uint32_t *__restrict__ table_ws,
-                                                              uint32_t total_chunks, uint32_t *__restrict__ tile_queue,
+                                                              uint32_t total_chunks, uint32_t *__restrict__ scratch_ws,
                                                               FilterTable ft) {
   using FT = Filt<DT>;
-  static_assert(!(CMP && CL), "live-key compaction and the claim layout do not combine");
   constexpr int KPT = 6;                    // keys per thread (C <= 6 * BLOCK)
   constexpr int VPT = (K * KPT + 3) / 4;    // 16-byte stores per thread per chunk, at most (CL: cap <= 4 * VPT * BLOCK)
   constexpr int SPI = (VPT + KPT - 1) / KPT;  // of those, per count iteration
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   const int tid = threadIdx.x;
-  if (blockIdx.x == 0 && tid == 0) *tile_queue = 0;  // pass B's tile queue
   const uint32_t C = a.C;
   const uint32_t TL = a.TL;
   const uint32_t tmask = (1u << TL) - 1u;
@@ -811,11 +793,10 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin16_kernel(BuildArgs a, Src key
   // CL: the second counter array and the two overflow flags follow the region
   uint32_t *hist2 = lpos + a.cap;
   uint32_t *oflag = hist2 + a.hist_words;
-  uint32_t *after = CL ? oflag + 4 : lpos + K * C;  // collapsed-key masks, pair table
+  uint32_t *after = CL ? oflag + 4 : lpos + K * C;  // the repeated-hash table
 
   const uint32_t G = gridDim.x;
-  const uint32_t slot =
-      (a.xcd_remap && G % 8 == 0) ? (blockIdx.x % 8) * (G / 8) + blockIdx.x / 8 : blockIdx.x;
+  const uint32_t slot = G % 8 == 0 ? (blockIdx.x % 8) * (G / 8) + blockIdx.x / 8 : blockIdx.x;
 
   // Every global load and store of the chunk loop below is issued
   // unconditionally (out-of-range lanes load a clamped key, and store to
@@ -823,7 +804,7 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin16_kernel(BuildArgs a, Src key
   // chunk c+1 waits only for its own keys (vmcnt(stores issued since)), not
   // for every outstanding store of chunk c-1 and the table (vmcnt(0)).
   const int wave = tid / kWave;
-  uint32_t *dummy = tile_queue + 64 + ((uint64_t)blockIdx.x * (BLOCK / kWave) + wave) * 4;
+  uint32_t *dummy = scratch_ws + kQueueWords + ((uint64_t)blockIdx.x * (BLOCK / kWave) + wave) * 4;
   uint4 *dummy4 = reinterpret_cast<uint4 *>(dummy);
   constexpr int TPT = (int)((kHistMax + BLOCK - 1) / BLOCK);  // table entries per thread, at most
 
@@ -844,17 +825,29 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin16_kernel(BuildArgs a, Src key
   // top of step c (no load in flight across the back-edge): 111 vs 127 us.
   Raw raw[KPT];
   uint32_t h1[KPT], h2[KPT];
-  if (slot >= total_chunks) return;
-  const bool hot_on = a.hot != 0;
-  uint32_t hotm = 0;  // bit i: key slot i collapsed (h1[i] holds its index; hash16h)
-  fetch(slot, raw);
-#pragma unroll
-  for (int i = 0; i < KPT; ++i) {
-    bool ht;
-    Src::hash_hot(raw[i], h1[i], h2[i], ht, hot_on);
-    hotm |= (uint32_t)ht << i;
+  // this workgroup's chunks c (wg), c+1 (n1) and c+2 (n2); DYN: from the
+  // queue, three ahead (thread 0 takes c+3 at the top of step c and publishes
+  // it in qa[] at the step's last barrier, so the atomic's latency is hidden)
+  uint32_t wg0 = slot, n1 = slot + G, n2 = slot + 2 * G;
+  uint32_t *qa = lds + (a.hist_words + 28);  // 2 words of the scan scratch's tail (scans use <= 17)
+  [[maybe_unused]] GroupQueue gq(scratch_ws, G, total_chunks);
+  if constexpr (DYN) {
+    if (tid == 0) {
+      qa[0] = gq.next();
+      qa[1] = gq.next();
+      qa[2] = gq.next();
+    }
+    __syncthreads();
+    wg0 = qa[0];
+    n1 = qa[1];
+    n2 = qa[2];
+    __syncthreads();  // read before qa is written again
   }
-  fetch(min(slot + G, total_chunks - 1), raw);
+  if (wg0 >= total_chunks) return;
+  fetch(wg0, raw);
+#pragma unroll
+  for (int i = 0; i < KPT; ++i) Src::hash(raw[i], h1[i], h2[i]);
+  fetch(min(n1, total_chunks - 1), raw);
   for (uint32_t i = tid; i < a.hist_words; i += BLOCK) hist[i] = 0;
   if constexpr (CL)
     for (uint32_t i = tid; i < a.hist_words + 4; i += BLOCK) hist2[i] = 0;  // and the flags
@@ -863,79 +856,25 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin16_kernel(BuildArgs a, Src key
   // an arithmetic shift and sign-extended bytes leave SplitMix keys only ~69 %
   // distinct (h1, h2) pairs at 10M keys, one pair 14 723 times.  A key whose
   // pair another key of this workgroup (same filter) already counted sets no
-  // new bit, so it is skipped.  dtab: 2^dd_log2 slots, claimed with a 64-bit
-  // compare-and-swap (EMPTY -> pair): a key is skipped only when its slot
-  // holds exactly its own pair, installed by a key that was counted.
-  // dd_mode 2: only keys whose seeds converged (h1 == h2: 39 % of the keys,
-  // 90 % of the repeats) claim, a 32-bit CAS of h1 into a table of twice the
-  // slots.
-  const uint32_t dd = a.dd_log2, dd2 = a.dd_mode == 2;
-  // With collapsed keys on, the first 2 * kHotN/32 words of that area are this
-  // workgroup's masks of the indices it met in its current and next filter
-  // (hpar selects the current one), and the pair table follows.
-  uint32_t *hmask = after;
-  unsigned long long *dtab = reinterpret_cast<unsigned long long *>(after + (hot_on ? 2 * kHotN / 32 : 0));
-  uint32_t *dtab32 = reinterpret_cast<uint32_t *>(dtab);
-  constexpr unsigned long long kEmpty = ~0ull;
+  // new bit, so it is skipped.  Only keys whose seeds converged (h1 == h2: 39 %
+  // of the keys, 90 % of the repeats) take part: each claims slot h1 >> (31 -
+  // dd) of a 2^(dd+1)-entry table with a 32-bit compare-and-swap (EMPTY ->
+  // h1), and a key is skipped only when its slot holds exactly its own h1,
+  // installed by a key that was counted.  (Every key claiming its 64-bit pair
+  // measured slower: DESIGN.md §4.)
+  const uint32_t dd = a.dd_log2;
+  uint32_t *dtab32 = after;
   if (dd)
-    for (uint32_t i = tid; i < (1u << dd); i += BLOCK) dtab[i] = kEmpty;
-  if (hot_on)
-    for (uint32_t i = tid; i < 2 * kHotN / 32; i += BLOCK) hmask[i] = 0;
-
-  // Compaction, phase 1 (chunk nwg hashed in h1/h2, hotm its collapsed slots):
-  // mark the collapsed keys in hmask[par], rank this thread's live keys in its
-  // wave and publish the wave's total in scratch[wave].  Phase 2, after a
-  // barrier: stage the live pairs densely at the start of lpos (which then
-  // holds no positions: each chunk's positions are stored out before its
-  // successor's keys are staged); returns the chunk's live keys.
-  const int lane = tid & (kWave - 1);
-  uint2 *lst = reinterpret_cast<uint2 *>(lpos);
-  auto rank_live = [&](uint32_t nwg, uint32_t par, uint32_t &off) -> uint32_t {
-    const auto &dn = FT::at(a, ft, FT::of_chunk(a, ft, nwg));
-    const uint32_t ncnt = min(C, dn.n - (nwg - dn.chunk_base) * C);
-    uint32_t v = 0;
-#pragma unroll
-    for (int i = 0; i < KPT; ++i)
-      if (tid + i * BLOCK < ncnt) v |= 1u << i;
-    uint32_t *hm = hmask + par * (kHotN / 32);
-#pragma unroll
-    for (int i = 0; i < KPT; ++i)
-      if ((v & hotm) >> i & 1u) atomicOr(&hm[h1[i] >> 5], 1u << (h1[i] & 31));
-    v &= ~hotm;
-    const uint32_t c = __builtin_popcount(v);
-    const uint32_t incl = wave_incl_scan(c, lane);
-    if (lane == kWave - 1) scratch[wave] = incl;
-    off = incl - c;
-    return v;
-  };
-  auto stage_live = [&](uint32_t v, uint32_t off) -> uint32_t {
-    uint32_t L = 0;
-#pragma unroll
-    for (int q = 0; q < BLOCK / kWave; ++q) {
-      const uint32_t t = scratch[q];
-      off += q < wave ? t : 0u;
-      L += t;
-    }
-#pragma unroll
-    for (int i = 0; i < KPT; ++i) {
-      if ((v >> i) & 1u) lst[off++] = make_uint2(h1[i], h2[i]);
-    }
-    return L;
-  };
-  uint32_t hpar = 0, nlive = 0;
-  if constexpr (CMP) {
-    __syncthreads();  // hmask cleared
-    uint32_t off;
-    const uint32_t v = rank_live(slot, 0, off);
-    __syncthreads();  // wave totals published
-    nlive = stage_live(v, off);
-  }
+    for (uint32_t i = tid; i < (2u << dd); i += BLOCK) dtab32[i] = ~0u;
 
   uint4 *pdst = dummy4;  // deferred store of the previous chunk
   uint32_t ptotal = 0;
   uint32_t par = 0;  // CL: counter array / overflow flag of this chunk
+  uint32_t qpar = 0;  // DYN: qa slot of this step
   STAMP_DECL
-  for (uint32_t wg = slot; wg < total_chunks; wg += G) {
+  for (uint32_t wg = wg0; wg < total_chunks;) {
+    [[maybe_unused]] uint32_t n3 = 0;
+    if (DYN && tid == 0) n3 = gq.next();  // used at this step's last barrier
     const int fcur = FT::of_chunk(a, ft, wg);
     const auto &d = FT::at(a, ft, fcur);
     const uint32_t w = wg - d.chunk_base;
@@ -945,35 +884,16 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin16_kernel(BuildArgs a, Src key
     uint32_t *hcur = hist, *hoth = hist2;
     if (CL && par) hcur = hist2, hoth = hist;
     const uint32_t tcap = CL ? (a.cap / T) & ~3u : 0u;  // slots per tile (the plan keeps it >= 4)
-    __syncthreads();  // hist cleared; the previous scatter is complete in lpos; the live keys staged
+    __syncthreads();  // hist cleared; the previous scatter is complete in lpos
     STAMP(0);
 
     // count(c) + store(c-1)
     const uint32_t pvec = ptotal >> 2;
     uint32_t live = 0;  // bit i: key slot i is counted
-    if constexpr (CMP) {  // dense slots: the staged live keys
 #pragma unroll
-      for (int i = 0; i < KPT; ++i) {
-        const uint32_t s = tid + i * BLOCK;
-        if (s < nlive) {
-          const uint2 v = lst[s];
-          h1[i] = v.x;
-          h2[i] = v.y;
-          live |= 1u << i;
-        }
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < KPT; ++i)
-        if (tid + i * BLOCK < cnt) live |= 1u << i;
-      if (hot_on) {  // a collapsed key marks its index and bins nothing
-#pragma unroll
-        for (int i = 0; i < KPT; ++i)
-          if ((live & hotm) >> i & 1u) atomicOr(&hmask[h1[i] >> 5], 1u << (h1[i] & 31));
-        live &= ~hotm;
-      }
-    }
-    if (dd && dd2) {
+    for (int i = 0; i < KPT; ++i)
+      if (tid + i * BLOCK < cnt) live |= 1u << i;
+    if (dd) {
       uint32_t old[KPT];
 #pragma unroll
       for (int i = 0; i < KPT; ++i) {
@@ -983,19 +903,6 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin16_kernel(BuildArgs a, Src key
 #pragma unroll
       for (int i = 0; i < KPT; ++i)
         if (old[i] != ~0u && old[i] == h1[i] && h1[i] == h2[i]) live &= ~(1u << i);
-    } else if (dd) {
-      unsigned long long old[KPT];
-#pragma unroll
-      for (int i = 0; i < KPT; ++i) {
-        const unsigned long long hv = ((unsigned long long)h2[i] << 32) | h1[i];
-        const uint32_t sl = (h1[i] + __builtin_amdgcn_alignbit(h2[i], h2[i], 16)) >> (32 - dd);
-        old[i] = (live >> i) & 1u ? atomicCAS(&dtab[sl], kEmpty, hv) : kEmpty;
-      }
-#pragma unroll
-      for (int i = 0; i < KPT; ++i) {
-        const unsigned long long hv = ((unsigned long long)h2[i] << 32) | h1[i];
-        if (old[i] != kEmpty && old[i] == hv) live &= ~(1u << i);
-      }
     }
     uint32_t pos[KPT][K];
 #pragma unroll
@@ -1012,7 +919,7 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin16_kernel(BuildArgs a, Src key
 #pragma unroll
           for (int j = 0; j < K; ++j) atomicAdd(&hist[pos[i][j] >> TL], 1u);
       }
-      if constexpr (!CMP && !CL) {
+      if constexpr (!CL) {
 #pragma unroll
         for (int sv = i * SPI; sv < (i + 1) * SPI && sv < VPT; ++sv) {
           const uint32_t v = tid + sv * BLOCK;
@@ -1024,7 +931,7 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin16_kernel(BuildArgs a, Src key
         }
       }
     }
-    if constexpr (!CMP && !CL) {
+    if constexpr (!CL) {
       const bool ok = (uint32_t)tid < (ptotal & 3u);
       *(ok ? reinterpret_cast<uint32_t *>(pdst) + pvec * 4 + tid : dummy) = lpos[ok ? pvec * 4 + tid : 0u];
     }
@@ -1034,8 +941,7 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin16_kernel(BuildArgs a, Src key
       __syncthreads();  // counts complete; the previous chunk's LDS copy is read out
       STAMP(1);
 
-      total = a.scan1 ? block_excl_scan_array_1b<BLOCK>(hist, T + 1, scratch)
-                      : block_excl_scan_array<BLOCK>(hist, T + 1, scratch);
+      total = block_excl_scan_array_1b<BLOCK>(hist, T + 1, scratch);
       STAMP(2);
 #pragma unroll
       for (int r = 0; r < TPT; ++r) {
@@ -1049,7 +955,6 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin16_kernel(BuildArgs a, Src key
 
     // scatter(c) + hash(c+1) (its keys arrived during the previous chunk;
     // lanes past the end hash a clamped key and never use the result)
-    uint32_t hotn = 0;
     bool ovf = false;  // CL: a position found its tile's slots taken
 #pragma unroll
     for (int i = 0; i < KPT; ++i) {
@@ -1076,20 +981,14 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin16_kernel(BuildArgs a, Src key
         h2[i] = raw[i].y | 1u;
       } else
 #endif
-      {
-        bool ht;
-        Src::hash_hot(raw[i], h1[i], h2[i], ht, hot_on);
-        hotn |= (uint32_t)ht << i;
-      }
+        Src::hash(raw[i], h1[i], h2[i]);
     }
-    hotm = hotn;
-    fetch(min(wg + 2 * G, total_chunks - 1), raw);
-    // the pair table and the index mask hold one filter's keys (positions depend on m)
-    const bool last_of_filter = wg + G >= total_chunks || FT::of_chunk(a, ft, wg + G) != fcur;
-    uint32_t nv = 0, noff = 0;
-    if (CMP && wg + G < total_chunks) nv = rank_live(wg + G, hpar ^ (uint32_t)last_of_filter, noff);
+    fetch(min(n2, total_chunks - 1), raw);
+    // the repeated-hash table holds one filter's keys (positions depend on m)
+    const bool last_of_filter = n1 >= total_chunks || FT::of_chunk(a, ft, n1) != fcur;
     if (CL && ovf) oflag[par] = 1u;
-    __syncthreads();  // lpos holds chunk c sorted; hist is free; this chunk's marks are in hmask
+    if (DYN && tid == 0) qa[qpar] = n3;
+    __syncthreads();  // lpos holds chunk c sorted; hist is free
     STAMP(4);
     if constexpr (CL) {
       // the other counter array and flag were last read before this chunk's
@@ -1099,19 +998,8 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin16_kernel(BuildArgs a, Src key
     } else {
       for (uint32_t i = tid; i <= T; i += BLOCK) hist[i] = 0;
     }
-    if (dd && last_of_filter && wg + G < total_chunks)
-      for (uint32_t i = tid; i < (1u << dd); i += BLOCK) dtab[i] = kEmpty;
-    if (hot_on && last_of_filter && tid < (int)(kHotN / 32)) {
-      // stamp the indices this workgroup met in filter fcur (every store
-      // issued, unmarked ones to the wave's scratch line) and clear the mask
-      uint32_t *hm = hmask + (CMP ? hpar : 0u) * (kHotN / 32);
-      const uint32_t mw = hm[tid];
-      hm[tid] = 0;
-      unsigned long long *st = reinterpret_cast<unsigned long long *>(a.stamps) + (uint64_t)fcur * kHotN + tid * 32u;
-#pragma unroll 8
-      for (int b = 0; b < 32; ++b)
-        *(((mw >> b) & 1u) ? st + b : reinterpret_cast<unsigned long long *>(dummy)) = a.nonce;
-    }
+    if (dd && last_of_filter && n1 < total_chunks)
+      for (uint32_t i = tid; i < (2u << dd); i += BLOCK) dtab32[i] = ~0u;
     if constexpr (CL) {
       uint4 *dst = reinterpret_cast<uint4 *>(pos_ws + d.pos_base + (uint64_t)w * a.cap);
       if (oflag[par] == 0u) {
@@ -1169,26 +1057,19 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin16_kernel(BuildArgs a, Src key
         *(ok ? reinterpret_cast<uint32_t *>(dst) + tv * 4 + tid : dummy) = lpos[ok ? tv * 4 + tid : 0u];
       }
       par ^= 1u;
-    } else if constexpr (CMP) {
-      hpar ^= (uint32_t)last_of_filter;
-      // this chunk's positions out of lpos now, then the next chunk's live keys in
-      uint4 *dst = reinterpret_cast<uint4 *>(pos_ws + d.pos_base + (uint64_t)w * a.cap);
-      const uint32_t tv = total >> 2;
-#pragma unroll
-      for (int sv = 0; sv < VPT; ++sv) {
-        const uint32_t v = tid + sv * BLOCK;
-        const bool ok = v < tv;
-        *(ok ? dst + v : dummy4) = src4[ok ? v : 0u];
-      }
-      {
-        const bool ok = (uint32_t)tid < (total & 3u);
-        *(ok ? reinterpret_cast<uint32_t *>(dst) + tv * 4 + tid : dummy) = lpos[ok ? tv * 4 + tid : 0u];
-      }
-      __syncthreads();  // lpos read out
-      if (wg + G < total_chunks) nlive = stage_live(nv, noff);
     } else {
       pdst = reinterpret_cast<uint4 *>(pos_ws + d.pos_base + (uint64_t)w * a.cap);
       ptotal = total;
+    }
+    // the next step: (qa[qpar] was published at this step's last barrier and
+    // is rewritten two steps on, after two more barriers)
+    wg = n1;
+    n1 = n2;
+    if constexpr (DYN) {
+      n2 = qa[qpar];
+      qpar ^= 1u;
+    } else {
+      n2 += G;
     }
   }
   // epilogue: the last chunk's store
@@ -1213,29 +1094,32 @@ __global__ __launch_bounds__(BLOCK) void bloom_bin16_kernel(BuildArgs a, Src key
 // while the current stage is ds_or_b32'd into the LDS tile.  The rare longer
 // segments (hot tiles) finish in a 4-deep unrolled loop.  The finished tile's
 // 16-byte stores drain while the next tile is zeroed.
-// HOT: pass A stamped collapsed keys (a.hot), whose bits this pass adds.
 // OCC: workgroups per CU the kernel is compiled for (2: at most 64 VGPRs, for
-// tiles whose LDS leaves room for two; ADL_BLOOM_B_OCC).
-template <int D, bool DT, bool HOT = false, int OCC = 1>
-__global__ __launch_bounds__(kBlockB, 4 * OCC) void bloom_tile_kernel(BuildArgs a,
+// tiles whose LDS leaves room for two).  DYN: tiles from the work queues (while
+// a resident probe server exists; two 1024-thread workgroups fill a CU's 32
+// wave slots, so on the server's CU one of them starts only at the end and
+// then finds the queues empty).
+template <int D, bool DT, int OCC = 1, bool DYN = false, int BLK = kBlockB>
+__global__ __launch_bounds__(BLK, 4 * OCC) void bloom_tile_kernel(BuildArgs a,
                                                              const uint32_t *__restrict__ pos_ws,
                                                              const uint32_t *__restrict__ table_ws,
                                                              uint8_t *__restrict__ bitmaps,
-                                                             uint32_t total_tiles, uint32_t *__restrict__ tile_queue,
+                                                             uint32_t total_tiles, uint32_t *__restrict__ scratch_ws,
                                                              FilterTable ft) {
   using FT = Filt<DT>;
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   const int tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid / kWave;
-  constexpr int NWAVES = kBlockB / kWave;
+  constexpr int NWAVES = BLK / kWave;
   // segment descriptors staged per batch (half at two workgroups per CU, so
   // a 2^19-bit tile and its batch fit twice in a CU's LDS)
-  constexpr int SEGB = OCC == 2 ? kSegBatch / 2 : kSegBatch;
-  constexpr int RPT = SEGB / kBlockB;  // table entries per thread per batch
+  constexpr int SEGB = OCC == 2 ? BLK : 2 * BLK;
+  static_assert(SEGB <= kSegBatch, "the plan's LDS holds kSegBatch descriptors");
+  constexpr int RPT = SEGB / BLK;  // table entries per thread per batch
   const uint32_t TL = a.TL;
   const uint32_t tile_words = 1u << (TL - 5);
   uint32_t *tile = lds;                                      // 2^TL bits
   uint2 *seg = reinterpret_cast<uint2 *>(lds + tile_words);  // SEGB {start word, length}
-  uint32_t *qs = lds + tile_words + 2 * SEGB;                // tile-queue broadcast (2 words)
+  uint32_t *qb = lds + tile_words + 2 * SEGB;                // DYN: 2 words, the tile after next
 
   auto fetch_rows = [&](uint32_t wg, uint32_t wb, uint32_t (&rs)[RPT], uint32_t (&re)[RPT]) {
     const auto &d = FT::at(a, ft, FT::of_tile(a, ft, wg));
@@ -1243,7 +1127,7 @@ __global__ __launch_bounds__(kBlockB, 4 * OCC) void bloom_tile_kernel(BuildArgs 
     const uint32_t *row0 = table_ws + d.table_base + (uint64_t)lt * W;
 #pragma unroll
     for (int r = 0; r < RPT; ++r) {
-      const uint32_t i = wb + tid + r * kBlockB;
+      const uint32_t i = wb + tid + r * BLK;
       rs[r] = re[r] = 0;
       if (i < W) {
         if (a.claim) {  // (start << 16) | length
@@ -1271,34 +1155,32 @@ __global__ __launch_bounds__(kBlockB, 4 * OCC) void bloom_tile_kernel(BuildArgs 
   // Round r covers tiles [r*G, (r+1)*G); inside a round each XCD takes G/8
   // consecutive tiles, so the line a tile's segment shares with its
   // neighbour's (segments of consecutive tiles are adjacent in every chunk
-  // region) is fetched into one L2 once.  Speed only.
-  // Tiles come either from a work queue (dynamic: a workgroup that finishes
-  // early takes the next tile, which evens out the hot tiles) or statically,
-  // round r covering tiles [r*G, (r+1)*G) with each XCD taking G/8
-  // consecutive tiles so the line a tile's segment shares with its
-  // neighbour's is fetched into one L2 once.  Speed only, either way.
+  // region) is fetched into one L2 once.  Speed only.  (A work queue of tiles,
+  // global or per XCD, measured slower than this static order.)
   const uint32_t G = gridDim.x;
-  uint32_t wg;
-  if (a.dyn_tiles) {
-    if (tid == 0) qs[0] = atomicAdd(tile_queue, 1u);
+  uint32_t wg = G % 8 == 0 ? (blockIdx.x % 8) * (G / 8) + blockIdx.x / 8 : blockIdx.x;
+  uint32_t nxt = wg + G;  // the tile after this one
+  // DYN: tiles from the queue (work queues above), two ahead: thread 0 takes
+  // the tile after next at the top of a tile and publishes it at its last barrier
+  [[maybe_unused]] GroupQueue gq(scratch_ws + 8 * 16, G, total_tiles);
+  uint32_t qpar = 0;
+  if constexpr (DYN) {
+    if (tid == 0) {
+      qb[0] = gq.next();
+      qb[1] = gq.next();
+    }
     __syncthreads();
-    wg = qs[0];
-  } else {
-    wg = (a.xcd_remap && G % 8 == 0) ? (blockIdx.x % 8) * (G / 8) + blockIdx.x / 8 : blockIdx.x;
+    wg = qb[0];
+    nxt = qb[1];
+    __syncthreads();  // read before qb is written again
   }
   uint32_t pre_s[RPT], pre_e[RPT];
   if (wg < total_tiles) fetch_rows(wg, 0, pre_s, pre_e);
   {  // the tile starts zeroed; every write-out re-zeroes it
     uint4 *t4w = reinterpret_cast<uint4 *>(tile);
-    for (uint32_t i = tid; i < tile_words / 4; i += kBlockB) t4w[i] = make_uint4(0, 0, 0, 0);
+    for (uint32_t i = tid; i < tile_words / 4; i += BLK) t4w[i] = make_uint4(0, 0, 0, 0);
   }
   STAMP_DECL
-
-  // Collapsed keys (a.hot): thread t holds the positions (j+1)*hot_h16(i) % m
-  // of indices i = t + q*kBlockB, computed once per divisor m.
-  constexpr int kHQ = HOT ? (int)(kHotN / kBlockB) : 1, kHotK = 6;  // pass A's collapsed-key path has k == 6
-  uint32_t hpos[kHQ][kHotK];
-  uint32_t hot_m = 0;  // m that hpos holds positions for (0: none yet)
 
   while (wg < total_tiles) {
     const int fi = FT::of_tile(a, ft, wg);
@@ -1306,29 +1188,10 @@ __global__ __launch_bounds__(kBlockB, 4 * OCC) void bloom_tile_kernel(BuildArgs 
     const uint32_t lt = wg - d.tile_base;
     const uint32_t W = d.chunks;
     const uint32_t pos_base = (uint32_t)d.pos_base;
-
-    if (a.dyn_tiles && tid == 0) qs[1] = atomicAdd(tile_queue, 1u);
-    __syncthreads();  // next tile index published
     STAMP(0);
-    if constexpr (HOT) {  // the bits of the collapsed keys pass A stamped for this filter
-      if (d.mod.m != hot_m) {
-        hot_m = d.mod.m;
-#pragma unroll
-        for (int q = 0; q < kHQ; ++q) {
-          const uint32_t F = hot_h16(tid + q * kBlockB);
-          uint32_t x = F;
-#pragma unroll
-          for (int j = 0; j < kHotK; ++j, x += F) hpos[q][j] = fastmod(x, d.mod);
-        }
-      }
-      const unsigned long long *st = reinterpret_cast<const unsigned long long *>(a.stamps) + (uint64_t)fi * kHotN;
-#pragma unroll
-      for (int q = 0; q < kHQ; ++q)
-#pragma unroll
-        for (int j = 0; j < kHotK; ++j)
-          if ((hpos[q][j] >> TL) == lt && st[tid + q * kBlockB] == a.nonce) or_pos(hpos[q][j] & ((1u << TL) - 1u));
-    }
-    const uint32_t next = a.dyn_tiles ? qs[1] : wg + G;
+    const uint32_t next = nxt;
+    [[maybe_unused]] uint32_t nn = 0;
+    if (DYN && tid == 0) nn = gq.next();  // the tile after next, published at this tile's last barrier
     // an empty filter (no chunks) has no batch to prefetch the next tile from
     if (W == 0 && next < total_tiles) fetch_rows(next, 0, pre_s, pre_e);
 
@@ -1343,7 +1206,7 @@ __global__ __launch_bounds__(kBlockB, 4 * OCC) void bloom_tile_kernel(BuildArgs 
       }
 #pragma unroll
       for (int r = 0; r < RPT; ++r) {
-        const uint32_t i = tid + r * kBlockB;
+        const uint32_t i = tid + r * BLK;
         if (i < nw) seg[i] = make_uint2(pos_base + (wb + i) * a.cap + rs[r], re[r] - rs[r]);
       }
       __syncthreads();  // segment list ready
@@ -1427,54 +1290,32 @@ __global__ __launch_bounds__(kBlockB, 4 * OCC) void bloom_tile_kernel(BuildArgs 
     // a short last tile), so the next tile needs no separate zeroing sweep.
     uint4 *t4z = reinterpret_cast<uint4 *>(tile);
     const uint32_t nvec = (uint32_t)(nbytes >> 4);
-    for (uint32_t i = tid; i < tile_words / 4; i += kBlockB) {
+    for (uint32_t i = tid; i < tile_words / 4; i += BLK) {
       const uint4 v = t4[i];
       t4z[i] = make_uint4(0, 0, 0, 0);
       if (i < nvec) {
 #ifdef ADL_BLOOM_STAMPS
         if (a.exp & 8) continue;
 #endif
-        if (a.nt_bitmap) store_nt(out4 + i, v);
-        else out4[i] = v;
+        store_nt(out4 + i, v);
       }
     }
+    if (DYN && tid == 0) qb[qpar] = nn;
     __syncthreads();  // the tile is read out and zero again
     STAMP(3);
     wg = next;
+    if constexpr (DYN) {
+      nxt = qb[qpar];
+      qpar ^= 1u;
+    } else {
+      nxt = next + G;
+    }
   }
 #ifdef ADL_BLOOM_STAMPS
-  if (exp_sink == 0x9e3779b9u) tile_queue[1] = exp_sink;  // keeps the diagnostic sum alive
+  if (exp_sink == 0x9e3779b9u) scratch_ws[kQueueWords] = exp_sink;  // keeps the diagnostic sum alive
 #endif
   STAMP_FLUSH(1);
 }
-
-// ---------------------------------------------------------------- direct atomics
-__global__ __launch_bounds__(256) void zero_kernel(uint4 *__restrict__ p, uint64_t n16) {
-  for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n16; i += (uint64_t)gridDim.x * 256)
-    p[i] = make_uint4(0, 0, 0, 0);
-}
-
-template <class Keys>
-__global__ __launch_bounds__(256) void bloom_atomic_kernel(Keys keys, uint64_t n, uint32_t k,
-                                                           FastMod mod, uint32_t *__restrict__ bitmap) {
-  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
-       i += (uint64_t)gridDim.x * blockDim.x) {
-    uint32_t h1, h2;
-    keys.hash(i, h1, h2);
-    for (uint32_t j = 0; j < k; ++j) {
-      const uint32_t p = fastmod(h1 + j * h2, mod);
-      const uint32_t word = p >> 5, bit = 1u << (p & 31);
-      // Test before the atomic: bits only ever go 0 -> 1 within the launch,
-      // so a set bit seen through a stale line is still set.
-      if (!(__builtin_nontemporal_load(bitmap + word) & bit)) atomicOr(bitmap + word, bit);
-    }
-  }
-}
-
-// A view of the key set starting at key `b` (used by the atomic path).
-inline Keys16 shift_keys(Keys16 k, uint64_t b) { k.keys += b; return k; }
-inline KeysStride shift_keys(KeysStride k, uint64_t b) { k.keys += b * k.stride; return k; }
-inline KeysVar shift_keys(KeysVar k, uint64_t b) { k.offs += b; return k; }
 
 // ---------------------------------------------------------------- host plan
 struct Plan {
@@ -1482,31 +1323,16 @@ struct Plan {
   std::vector<FilterDesc> f;  // every filter's descriptor (a.f holds them too when nf <= kMaxFilters)
   bool dt = false;            // more than kMaxFilters: descriptors in the workspace's FilterTable
   uint64_t pos_words = 0, table_words = 0, scratch_words = 0, hash_words = 0, ft_bytes = 0, ws_bytes = 0;
-  uint64_t stamp_off = 0;  // byte offset of the collapsed-key stamps (kHotN u64 per filter)
-  bool hot = false;        // collapsed keys stamped, not binned (16-byte keys, k = 6; ADL_BLOOM_HOT)
-  bool compact = false;    // with hot: pass A compacts the live keys (ADL_BLOOM_COMPACT)
-  bool claim = false;      // claim layout sizes (ADL_BLOOM_CLAIM): bloom_bin16_kernel<..., CL> runs
+  bool claim = false;      // claim layout sizes: bloom_bin16_kernel<..., CL> runs
   uint32_t total_chunks = 0, total_tiles = 0, total_sc = 0;
   uint32_t grid_a = 0, grid_b = 0;  // persistent grids
-  uint32_t occ_b = 1;               // pass-B workgroups per CU (ADL_BLOOM_B_OCC)
-  uint32_t block_a = 512;             // pass A threads per workgroup
-  uint32_t depth = kDepthB;           // pass B descriptors per step
-  bool sequential_a = false;          // ADL_BLOOM_SEQ_A=1: the unpipelined pass A (A/B tuning)
+  uint32_t occ_b = 1;               // pass-B workgroups per CU
   size_t lds_a = 0, lds_b = 0;
 };
 
-uint32_t env_flag(const char *name, uint32_t dflt) {
-  const char *e = getenv(name);
-  return e ? (uint32_t)(atoi(e) != 0) : dflt;
-}
-
-uint32_t env_u32(const char *name, uint32_t dflt) {
-  const char *e = getenv(name);
-  return e ? (uint32_t)atoi(e) : dflt;
-}
-
 int make_plan(const uint64_t *counts, uint32_t nf, int32_t bpk, Plan &p) {
   if (nf == 0 || bpk < 0) return ADL_ERR_INVALID_ARG;
+  const adl_host::Knobs &kn = adl_host::knobs();
   memset(&p.a, 0, sizeof(p.a));
   p.f.assign(nf, FilterDesc{});
   p.dt = nf > (uint32_t)kMaxFilters;
@@ -1537,11 +1363,8 @@ int make_plan(const uint64_t *counts, uint32_t nf, int32_t bpk, Plan &p) {
   // A's atomics, and such tiles leave LDS for two pass-B workgroups per CU
   // (below).  Measured on configs[3]: 3.66-3.68 ms at 2^18 bits with two
   // per CU, 4.06-4.11 at 2^20 (profiles/r04/ab_tile_size_occ.log).
-  bool tl_set = false;
-  if (const char *e = getenv("ADL_BLOOM_TILE_LOG2")) {  // tuning override
-    const int v = atoi(e);
-    if (v >= (int)kMinTileLog2 && v <= (int)kMaxTileLog2) TL = (uint32_t)v, tl_set = true;
-  }
+  const bool tl_set = kn.tile_log2 >= kMinTileLog2 && kn.tile_log2 <= kMaxTileLog2;  // test / tuning override
+  if (tl_set) TL = kn.tile_log2;
   if (!tl_set && k == 6)
     while (TL > 18 && tiles_at(TL, true) < kFewTiles && (uint64_t)k * kChunkEst >= kMinRun * tiles_at(TL - 1, true))
       --TL;
@@ -1549,22 +1372,18 @@ int make_plan(const uint64_t *counts, uint32_t nf, int32_t bpk, Plan &p) {
   const uint32_t hist_words = (uint32_t)adl_host::round_up(tiles_at(TL, true) + 1, 4);
 
   // Keys per chunk: as many as the rest of the pass-A LDS holds, then evened
-  // out so the chunks split into whole rounds of the persistent grid.
-  // Pass A geometry (ADL_BLOOM_A_WGS_PER_CU): 2 x 512 threads per CU overlap
-  // one workgroup's hashing with the other's LDS sort; 1 x 1024 threads per
-  // CU doubles the chunk, so pass B gathers half as many, twice as long
-  // segments.
+  // out so the chunks split into whole rounds of the persistent grid (one
+  // 1024-thread workgroup per CU: measured against two 512-thread ones, the
+  // longer chunks halve pass B's segments).
   const uint32_t cus = adl_host::device_cus();
-  const uint32_t bpc = env_u32("ADL_BLOOM_A_WGS_PER_CU", 1) == 2 ? 2 : 1;
-  const uint32_t block_a = bpc == 1 ? 1024 : 512;
-  const uint32_t grid_a_max = bpc * cus;
+  const uint32_t grid_a_max = cus;
   const uint32_t kpt = k == 6 ? 6 : kKptMax;
-  const uint32_t lds_words_a = kLdsWordsPerCu / bpc - (bpc == 1 ? 256 : 0);
+  const uint32_t lds_words_a = kLdsWordsPerCu - kLdsReserveWords;
   // LDS: tile counters + scan scratch + k*C positions + C key indices and 256
   // length classes (the length sort of variable-length keys; reserved for every
   // key shape so the workspace size does not depend on it)
   const uint32_t cmax =
-      std::min<uint32_t>(block_a * kpt, (lds_words_a - hist_words - 32 - 256) / (k + 1)) & ~3u;
+      std::min<uint32_t>(kBlockA * kpt, (lds_words_a - hist_words - 32 - 256) / (k + 1)) & ~3u;
   if (cmax < 4) return ADL_ERR_TOO_LARGE;
   // chunks of C keys over all filters (each filter's last chunk is partial)
   auto nchunks = [&](uint64_t c) {
@@ -1587,39 +1406,36 @@ int make_plan(const uint64_t *counts, uint32_t nf, int32_t bpk, Plan &p) {
     }
     return c;
   };
-  // Claim layout (ADL_BLOOM_CLAIM; 16-byte keys and hashed pairs with k = 6,
-  // not with collapsed-key stamping): the region of cap words gives each tile
-  // of a filter cap / T slots.  C shrinks so the region holds k*C positions
-  // times the slack (ADL_BLOOM_CLAIM_SLACK, percent); the layout is kept only
-  // if the largest filter's share per tile clears its mean run by
-  // ADL_BLOOM_CLAIM_SIGMA standard deviations (Poisson), so overflowing chunks
-  // (sorted exactly, more slowly) stay rare.  The region takes all the LDS
-  // left over (fewer overflows); ADL_BLOOM_CLAIM_CAP (percent of k*C) caps it
-  // and ADL_BLOOM_CLAIM=2 skips the share test: the tests force overflowing
-  // chunks that way.  Default (unset): only filters of at most kClaimTiles
-  // tiles, where it measured faster (pass A + B: 512 x 5 K keys 119 against
-  // 164 us, 256 x 10 K 92 / 109, 256 x 20 K 124 / 143, 128 x 30 K 94 / 101;
-  // 128 x 60 K and 32 x 100 K equal; 256 x 40 K and 64 x 300 K 4-11 % slower;
+  // Claim layout (16-byte keys and hashed pairs with k = 6): the region of cap
+  // words gives each tile of a filter cap / T slots.  C shrinks so the region
+  // holds k*C positions times kClaimSlack percent; the layout is kept only if
+  // the largest filter's share per tile clears its mean run by kClaimSigma
+  // standard deviations (Poisson), so overflowing chunks (sorted exactly, more
+  // slowly) stay rare.  The region takes all the LDS left over (fewer
+  // overflows); ADL_BLOOM_CLAIM_CAP (percent of k*C) caps it and
+  // ADL_BLOOM_CLAIM=2 skips the share test: the tests force overflowing
+  // chunks that way.  Default (3): only filters of at most kClaimTiles tiles,
+  // where it measured faster (pass A + B: 512 x 5 K keys 119 against 164 us,
+  // 256 x 10 K 92 / 109, 256 x 20 K 124 / 143, 128 x 30 K 94 / 101; 128 x 60 K
+  // and 32 x 100 K equal; 256 x 40 K and 64 x 300 K 4-11 % slower;
   // profiles/r04/ab_claim_shapes.log, ab_claim_threshold.log).
-  const uint32_t claim_mode = env_u32("ADL_BLOOM_CLAIM", 3);
-  bool claim = k == 6 && env_flag("ADL_BLOOM_HOT", 0) == 0 && claim_mode != 0;
+  const uint32_t claim_mode = kn.claim;
+  bool claim = k == 6 && claim_mode != 0;
   const int64_t room_cl = (int64_t)lds_words_a - 2 * hist_words - 36 - 256;  // region + C
   uint32_t cap_cl = 0;
   uint32_t C = 0;
   if (claim && room_cl > 64) {
-    const uint32_t slack = std::max<uint32_t>(env_u32("ADL_BLOOM_CLAIM_SLACK", 125), 100);
-    const uint32_t cm = std::min<uint32_t>(block_a * kpt, (uint32_t)(room_cl * 100 / (slack * k + 100))) & ~3u;
+    const uint32_t cm = std::min<uint32_t>(kBlockA * kpt, (uint32_t)(room_cl * 100 / (kClaimSlack * k + 100))) & ~3u;
     if (cm >= 4) {
       C = pick_c(cm);
-      int64_t cw = std::min<int64_t>(room_cl - C, 36ll * block_a);  // <= 4 * VPT * BLOCK
-      if (const uint32_t pct = env_u32("ADL_BLOOM_CLAIM_CAP", 0))
-        cw = std::min<int64_t>(cw, (int64_t)k * C * std::max<uint32_t>(pct, 100) / 100 + 3);
+      int64_t cw = std::min<int64_t>(room_cl - C, 36ll * kBlockA);  // <= 4 * VPT * BLOCK
+      if (kn.claim_cap) cw = std::min<int64_t>(cw, (int64_t)k * C * std::max<uint32_t>(kn.claim_cap, 100) / 100 + 3);
       cap_cl = (uint32_t)cw & ~3u;
       const uint32_t tmax = (uint32_t)tiles_at(TL, true);
       const uint32_t tcap = (cap_cl / tmax) & ~3u;
       const double mu = (double)k * C / tmax;
-      const double sig = env_u32("ADL_BLOOM_CLAIM_SIGMA", 4);
-      claim = cap_cl >= k * C && tcap >= 16 && (claim_mode == 2 || tcap >= mu + sig * std::sqrt(mu) + 8) &&
+      claim = cap_cl >= k * C && tcap >= 16 &&
+              (claim_mode == 2 || tcap >= mu + kClaimSigma * std::sqrt(mu) + 8) &&
               (claim_mode != 3 || tmax <= kClaimTiles);
     } else {
       claim = false;
@@ -1629,36 +1445,17 @@ int make_plan(const uint64_t *counts, uint32_t nf, int32_t bpk, Plan &p) {
   }
   if (!claim) C = pick_c(cmax);
   p.a.nf = nf;
-  p.a.xcd_remap = env_flag("ADL_BLOOM_XCD_REMAP", 1);
-  p.a.nt_keys = env_flag("ADL_BLOOM_NT_KEYS", 1);
-  p.a.nt_bitmap = env_flag("ADL_BLOOM_NT_BITMAP", 1);
-  p.a.dyn_tiles = env_flag("ADL_BLOOM_DYN_TILES", 0);
-  p.a.stage_keys = env_flag("ADL_BLOOM_STAGE_KEYS", 1);
-  p.a.scan1 = env_flag("ADL_BLOOM_SCAN1", 1);
-  p.a.var_hash = env_flag("ADL_BLOOM_VAR_HASH", 1);
+  p.a.stage_keys = 1;
   {
-    // pair table in the C + 256 words pass A reserves past the positions
-    // (the var-len length sort's area; bloom_bin16_kernel does not use it)
-    // (after the collapsed-key masks' 2 * kHotN / 32 words)
-    const uint32_t lg_max = std::min<uint32_t>(env_u32("ADL_BLOOM_DD_LOG2", 11), 12);
+    // the repeated-hash table sits in the C + 256 words pass A reserves past
+    // the positions (the var-len length sort's area; bloom_bin16_kernel does
+    // not use it there): 2^(lg+1) u32 slots
     uint32_t lg = 0;
-    while (lg < lg_max && (2u << (lg + 1)) <= C + 256 - 2 * kHotN / 32) ++lg;
-    p.a.dd_log2 = (env_flag("ADL_BLOOM_HASH_DEDUP", 1) && lg >= 4) ? lg : 0;
-    p.a.dd_mode = env_u32("ADL_BLOOM_DD_MODE", 2) == 1 ? 1 : 2;
-  }
-  // collapsed-key stamping and live-key compaction: bit-exact, measured slower
-  // than binning every key, so opt-in
-  p.hot = env_flag("ADL_BLOOM_HOT", 0) != 0;
-  p.compact = p.hot && env_flag("ADL_BLOOM_COMPACT", 0) != 0;
-  {
-    const uint32_t hk = env_u32("ADL_BLOOM_HV_KEYS", 512);
-    p.a.hv_keys = hk <= 256 ? 256 : hk <= 512 ? 512 : hk <= 1024 ? 1024 : 2048;
-    p.a.hv_split = env_u32("ADL_BLOOM_HV_SPLIT", 0);
+    while (lg < kDdLog2Max && (2u << (lg + 1)) <= C + 256) ++lg;
+    p.a.dd_log2 = (kn.hash_dedup && lg >= 4) ? lg : 0;
   }
 #ifdef ADL_BLOOM_STAMPS
-  p.a.exp = env_u32("ADL_BLOOM_EXP", 0);  // diagnostics build only
-#else
-  p.a.exp = 0;
+  p.a.exp = kn.exp;  // diagnostics build only
 #endif
   p.a.k = k;
   p.a.C = C;
@@ -1682,7 +1479,7 @@ int make_plan(const uint64_t *counts, uint32_t nf, int32_t bpk, Plan &p) {
     d.chunk_base = chunk;
     d.tile_base = tile;
     d.sc_base = sc;
-    sc += (uint32_t)((counts[f] + p.a.hv_keys - 1) / p.a.hv_keys);
+    sc += (uint32_t)((counts[f] + kHvKeys - 1) / kHvKeys);
     d.pos_base = pos;
     d.table_base = tab;
     d.bitmap_off = boff;  // overwritten by the caller
@@ -1699,55 +1496,35 @@ int make_plan(const uint64_t *counts, uint32_t nf, int32_t bpk, Plan &p) {
   p.total_sc = sc;
   p.pos_words = adl_host::round_up(pos, 64);
   p.table_words = adl_host::round_up(tab + kTablePad, 64);
-  // after the table: pass B's tile queue (64 words), then one 16-byte scratch
-  // line per pass-A wave (bloom_bin16_kernel's masked-off stores)
-  p.scratch_words = 64 + (uint64_t)grid_a_max * (block_a / kWave) * 4;
+  // after the table: the work-queue counters (GroupQueue), then one 16-byte
+  // scratch line per pass-A wave (bloom_bin16_kernel's masked-off stores)
+  p.scratch_words = adl_host::round_up(kQueueWords + (uint64_t)grid_a_max * (kBlockA / kWave) * 4 + 4, 64);
   // then (h1, h2) per key in the chunk grid: hash_var_kernel -> pass A
   // (variable-length keys; reserved for every key shape so the workspace size
   // does not depend on it)
   p.hash_words = adl_host::round_up(2ull * chunk * C, 64);
   // then (more than kMaxFilters) the FilterTable: descriptors, chunk / tile / run maps
   p.ft_bytes = p.dt ? adl_host::round_up(nf * sizeof(FilterDesc), 256) + 4ull * (chunk + tile + sc) + 256 : 0;
-  p.stamp_off = adl_host::round_up((p.pos_words + p.table_words + p.scratch_words + p.hash_words) * 4 + p.ft_bytes, 256);
-  p.ws_bytes = p.stamp_off + (uint64_t)nf * kHotN * 8 + 256;
+  p.ws_bytes = (p.pos_words + p.table_words + p.scratch_words + p.hash_words) * 4 + p.ft_bytes + 256;
   p.lds_a = claim ? (size_t)(2 * hist_words + 36 + cap + C + 256) * 4 : (size_t)(hist_words + 32 + (k + 1) * C + 256) * 4;
   p.lds_b = (size_t)((1u << (TL - 5)) + 2 * kSegBatch + 4) * 4;
   p.grid_a = std::min<uint32_t>(p.total_chunks, grid_a_max);
-  p.block_a = block_a;
-  p.depth = env_u32("ADL_BLOOM_DEPTH", kDepthB);
-  p.sequential_a = env_flag("ADL_BLOOM_SEQ_A", 0) != 0;
-  // Two pass-B workgroups per CU (64-VGPR kernels, half the segment batch)
-  // when the tile leaves room for two in LDS and the runs per tile are long:
-  // more waves to hide the gathers.  On the headline's 2^20-bit tiles it
-  // does not fit; forced at 2^19 there it is slower (short runs: 101 vs 68
-  // us).  ADL_BLOOM_B_OCC = 1 / 2 overrides.
+  // Two pass-B workgroups per CU (64-VGPR kernels, half the segment batch,
+  // pipeline depth 4) when the tile leaves room for two in LDS and the runs per
+  // tile are long: more waves to hide the gathers.  On the headline's
+  // 2^20-bit tiles it does not fit; forced at 2^19 there it is slower (short
+  // runs: 101 vs 68 us).
   {
     const size_t lds2 = (size_t)((1u << (TL - 5)) + kSegBatch + 4) * 4;
-    const uint32_t want = env_u32("ADL_BLOOM_B_OCC", 0);
     const bool long_runs = (uint64_t)k * C >= (uint64_t)kMinRun * tiles_at(TL, true);
-    bool two = want == 2 || (want == 0 && long_runs);
-    // (the stamped-keys pass B keeps one per CU: its index tables need the registers)
-    two = two && lds2 <= 80 * 1024 && !p.hot;
-    p.occ_b = two ? 2 : 1;
-    if (two) {
-      p.lds_b = lds2;
-      if (!getenv("ADL_BLOOM_DEPTH")) p.depth = 4;  // measured best at two per CU
-    }
+    p.occ_b = long_runs && lds2 <= 78 * 1024 ? 2 : 1;
+    if (p.occ_b == 2) p.lds_b = lds2;
   }
   p.grid_b = std::min<uint32_t>(p.total_tiles, p.occ_b * cus);
-  if (adl_host::env_on("ADL_BLOOM_DEBUG", false))
-    fprintf(stderr,
-            "adl_bloom plan: filters %u, tile 2^%u bits, tiles %u, C %u, chunks %u, region %u words%s, pass B %u per CU, "
-            "depth %u\n",
-            nf, TL, p.total_tiles, C, p.total_chunks, cap, claim ? " (claim)" : "", p.occ_b, p.depth);
+  if (kn.debug)
+    fprintf(stderr, "adl_bloom plan: filters %u, tile 2^%u bits, tiles %u, C %u, chunks %u, region %u words%s, pass B %u per CU\n",
+            nf, TL, p.total_tiles, C, p.total_chunks, cap, claim ? " (claim)" : "", p.occ_b);
   return ADL_OK;
-}
-
-// ADL_BLOOM_BUILD_ALGO=atomic selects the direct-atomic build (cross-check and
-// tuning; read per call so tests can switch it).
-bool use_atomic_path() {
-  const char *e = getenv("ADL_BLOOM_BUILD_ALGO");
-  return e && strcmp(e, "atomic") == 0;
 }
 
 // ---------------------------------------------------------------- instrumentation
@@ -1769,23 +1546,6 @@ inline hipEvent_t *prof_slot() {
   return &t_prof.ev[4 * t_prof.used++];
 }
 
-// A value unique to each launch pair of this process (and, by its random
-// start, to this process): pass A stamps collapsed-key indices with it, and
-// pass B accepts exactly the stamps equal to it, so the stamp area needs no
-// clearing and stamps of earlier builds in the same workspace never count.
-uint64_t next_nonce() {
-  static std::atomic<uint64_t> ctr{[] {
-    std::random_device rd;
-    uint64_t v = ((uint64_t)rd() << 32) ^ rd() ^
-                 (uint64_t)std::chrono::steady_clock::now().time_since_epoch().count() * 0x9e3779b97f4a7c15ull;
-    return v | 1u;
-  }()};
-  uint64_t v;
-  do v = ctr.fetch_add(0x9e3779b97f4a7c15ull * 2, std::memory_order_relaxed);
-  while (v == 0 || v == ~0ull);
-  return v;
-}
-
 // pass A of this thread's last launch pair wrote the claim layout's table
 // (adl_bloom_build_positions reads it)
 thread_local bool t_last_claim = false;
@@ -1793,27 +1553,28 @@ thread_local bool t_last_claim = false;
 template <bool DT, class Keys>
 int launch_binned_dt(const Plan &p, Keys keys, uint8_t *d_bitmaps, void *ws, hipStream_t st) {
   BuildArgs aa = p.a;
-  aa.stamps = reinterpret_cast<uint64_t *>(reinterpret_cast<uint8_t *>(ws) + p.stamp_off);
-  aa.nonce = next_nonce();
-  aa.hot = 0;
-  aa.compact = 0;
   aa.claim = 0;
-  uint32_t hot_used = 0;  // pass A stamped collapsed keys: pass B adds their bits
   uint32_t claim_used = 0;  // pass A wrote the claim layout's table entries
   uint32_t *pos_ws = reinterpret_cast<uint32_t *>(ws);
   uint32_t *tab_ws = pos_ws + p.pos_words;
-  uint32_t *queue = tab_ws + p.table_words;  // pass B tile queue, then pass A's scratch lines
-  uint2 *hp = reinterpret_cast<uint2 *>(queue + p.scratch_words);
+  uint32_t *scr = tab_ws + p.table_words;  // the work-queue counters, pass A's per-wave scratch lines
+  uint2 *hp = reinterpret_cast<uint2 *>(scr + p.scratch_words);
+  // While a resident probe server exists (a reader process), the passes take
+  // their chunks / tiles from the work queues: a workgroup slowed or held back
+  // by the server's wave on its CU then takes less work instead of holding up
+  // the pass (reads beside builds).  The counters start at 0.
+  const bool live = adl_srv::live_servers() > 0;
+  const bool dyn_a = live && p.grid_a % 8 == 0, dyn_b = live && p.grid_b % 8 == 0;
+  if (dyn_a || dyn_b) ADL_HIP_TRY(hipMemsetAsync(scr, 0, kQueueWords * 4, st));
   FilterTable ft{};
   if constexpr (DT) {
     // the descriptors go up in stream order; the maps are filled on the device
-    uint8_t *fbase = reinterpret_cast<uint8_t *>(queue + p.scratch_words + p.hash_words);
+    uint8_t *fbase = reinterpret_cast<uint8_t *>(scr + p.scratch_words + p.hash_words);
     FilterDesc *fd = reinterpret_cast<FilterDesc *>(fbase);
     uint32_t *chunk_f = reinterpret_cast<uint32_t *>(fbase + adl_host::round_up(p.f.size() * sizeof(FilterDesc), 256));
     uint32_t *tile_f = chunk_f + p.total_chunks, *sc_f = tile_f + p.total_tiles;
     if (int rc = adl_host::t_upload.upload(fd, p.f.data(), p.f.size() * sizeof(FilterDesc), st)) return rc;
-    hipLaunchKernelGGL(fill_maps_kernel, dim3((uint32_t)p.f.size()), dim3(256), 0, st, fd, chunk_f, tile_f, sc_f,
-                       p.a.hv_keys);
+    hipLaunchKernelGGL(fill_maps_kernel, dim3((uint32_t)p.f.size()), dim3(256), 0, st, fd, chunk_f, tile_f, sc_f);
     ADL_HIP_TRY(hipGetLastError());
     ft.fd = (cptr<FilterDesc>)fd;
     ft.chunk_f = (cptr<uint32_t>)chunk_f;
@@ -1828,105 +1589,83 @@ int launch_binned_dt(const Plan &p, Keys keys, uint8_t *d_bitmaps, void *ws, hip
   if (p.total_chunks) {
     // lim: lds_limit<kern>; the hashing pass (var-len keys) before pass A opens
     // the profiled pass-A interval instead of it
-    auto go_src = [&](auto lim, auto kern, const BuildArgs &args, auto src, bool hashed) -> int {
+    auto go16 = [&](auto lim, auto kern, const BuildArgs &args, auto src, bool hashed) -> int {
       if (int rc = lim()) return rc;
-      hipExtLaunchKernelGGL(kern, dim3(p.grid_a), dim3(p.block_a), p.lds_a, st,
-                            ev && !hashed ? ev[0] : nullptr, ev ? ev[1] : nullptr, 0, args, src, pos_ws, tab_ws,
-                            p.total_chunks, queue, ft);
+      hipExtLaunchKernelGGL(kern, dim3(p.grid_a), dim3(kBlockA), p.lds_a, st, ev && !hashed ? ev[0] : nullptr,
+                            ev ? ev[1] : nullptr, 0, args, src, pos_ws, tab_ws, p.total_chunks, scr, ft);
       ADL_HIP_TRY(hipGetLastError());
       return ADL_OK;
     };
-    auto by_block = [&](auto bt) -> int {  // bt: tag type carrying BLOCK
-      constexpr int B = decltype(bt)::value;
-      if constexpr (std::is_same<Keys, Keys16>::value) {
-        if (p.a.k == 6 && !p.sequential_a && !p.a.dedup) {
-          BuildArgs ah = aa;
-          ah.hot = hot_used = p.hot ? 1u : 0u;
-          if (p.compact) {
-            ah.compact = 1;
-            return go_src(adl_host::lds_limit<bloom_bin16_kernel<B, 6, Src16, DT, true>>,
-                          bloom_bin16_kernel<B, 6, Src16, DT, true>, ah, Src16{keys.keys}, false);
-          }
-          if (p.claim) {
-            ah.claim = claim_used = 1;
-            return go_src(adl_host::lds_limit<bloom_bin16_kernel<B, 6, Src16, DT, false, true>>,
-                          bloom_bin16_kernel<B, 6, Src16, DT, false, true>, ah, Src16{keys.keys}, false);
-          }
-          return go_src(adl_host::lds_limit<bloom_bin16_kernel<B, 6, Src16, DT>>, bloom_bin16_kernel<B, 6, Src16, DT>,
-                        ah, Src16{keys.keys}, false);
-        }
-      }
-      if constexpr (std::is_same<Keys, KeysVar>::value) {
-        // length-sorted hashing pass, then pass A over the (h1, h2) pairs; the
-        // profiled pass-A interval spans both launches
-        if (p.a.k == 6 && p.a.var_hash && !p.sequential_a && !p.a.dedup) {
-          auto hv_go = [&](auto lim, auto kern, size_t lds) -> int {
-            if (int rc = lim()) return rc;
-            hipExtLaunchKernelGGL(kern, dim3(p.total_sc), dim3(kHvBlock), lds, st, ev ? ev[0] : nullptr, nullptr, 0,
-                                  aa, keys, hp, p.total_sc, ft);
-            ADL_HIP_TRY(hipGetLastError());
-            return ADL_OK;
-          };
-          const int rh = p.a.hv_keys == 256
-                             ? hv_go(adl_host::lds_limit<hash_var_kernel<256, DT>>, hash_var_kernel<256, DT>,
-                                     hv_lds_bytes<256>())
-                         : p.a.hv_keys == 512
-                             ? hv_go(adl_host::lds_limit<hash_var_kernel<512, DT>>, hash_var_kernel<512, DT>,
-                                     hv_lds_bytes<512>())
-                         : p.a.hv_keys == 1024
-                             ? hv_go(adl_host::lds_limit<hash_var_kernel<1024, DT>>, hash_var_kernel<1024, DT>,
-                                     hv_lds_bytes<1024>())
-                             : hv_go(adl_host::lds_limit<hash_var_kernel<2048, DT>>, hash_var_kernel<2048, DT>,
-                                     hv_lds_bytes<2048>());
-          if (rh) return rh;
-          // the pair table pays for 16-byte keys only (configs[2]'s keys repeat few pairs:
-          // pass B 64 -> 70 us with it)
-          BuildArgs av = aa;
-          av.dd_log2 = 0;
-          if (p.claim) {
-            av.claim = claim_used = 1;
-            return go_src(adl_host::lds_limit<bloom_bin16_kernel<B, 6, SrcH, DT, false, true>>,
-                          bloom_bin16_kernel<B, 6, SrcH, DT, false, true>, av, SrcH{hp, p.a.C}, true);
-          }
-          return go_src(adl_host::lds_limit<bloom_bin16_kernel<B, 6, SrcH, DT>>, bloom_bin16_kernel<B, 6, SrcH, DT>,
-                        av, SrcH{hp, p.a.C}, true);
-        }
-      }
-      if (p.a.k == 6)
-        return go_src(adl_host::lds_limit<bloom_bin_kernel<B, 6, 6, Keys, DT>>, bloom_bin_kernel<B, 6, 6, Keys, DT>,
-                      aa, keys, false);
-      return go_src(adl_host::lds_limit<bloom_bin_kernel<B, 0, kKptMax, Keys, DT>>,
-                    bloom_bin_kernel<B, 0, kKptMax, Keys, DT>, aa, keys, false);
+    auto go = [&](auto lim, auto kern) -> int {
+      if (int rc = lim()) return rc;
+      hipExtLaunchKernelGGL(kern, dim3(p.grid_a), dim3(kBlockA), p.lds_a, st, ev ? ev[0] : nullptr,
+                            ev ? ev[1] : nullptr, 0, aa, keys, pos_ws, tab_ws, p.total_chunks, ft);
+      ADL_HIP_TRY(hipGetLastError());
+      return ADL_OK;
     };
-    const int rc = p.block_a == 1024 ? by_block(std::integral_constant<int, 1024>{})
-                                     : by_block(std::integral_constant<int, 512>{});
+    constexpr int B = (int)kBlockA;
+    // bloom_bin16_kernel in the claim layout or not, its chunks from the work
+    // queues or in the static order
+    auto bin16 = [&](auto src, BuildArgs args, bool hashed) -> int {
+      using S = decltype(src);
+      if (p.claim) {
+        args.claim = claim_used = 1;
+        if (dyn_a)
+          return go16(adl_host::lds_limit<bloom_bin16_kernel<B, 6, S, DT, true, true>>,
+                      bloom_bin16_kernel<B, 6, S, DT, true, true>, args, src, hashed);
+        return go16(adl_host::lds_limit<bloom_bin16_kernel<B, 6, S, DT, true>>, bloom_bin16_kernel<B, 6, S, DT, true>,
+                    args, src, hashed);
+      }
+      if (dyn_a)
+        return go16(adl_host::lds_limit<bloom_bin16_kernel<B, 6, S, DT, false, true>>,
+                    bloom_bin16_kernel<B, 6, S, DT, false, true>, args, src, hashed);
+      return go16(adl_host::lds_limit<bloom_bin16_kernel<B, 6, S, DT>>, bloom_bin16_kernel<B, 6, S, DT>, args, src,
+                  hashed);
+    };
+    int rc = -1;
+    if constexpr (std::is_same<Keys, Keys16>::value) {
+      if (p.a.k == 6 && !p.a.dedup) rc = bin16(Src16{keys.keys}, aa, false);
+    }
+    if constexpr (std::is_same<Keys, KeysVar>::value) {
+      // length-sorted hashing pass, then pass A over the (h1, h2) pairs; the
+      // profiled pass-A interval spans both launches.  (Adjacent-duplicate
+      // skipping needs the keys in order: the generic pass A below.)
+      if (p.a.k == 6 && p.a.stage_keys && !p.a.dedup) {
+        if (int r = adl_host::lds_limit<hash_var_kernel<kHvKeys, DT>>()) return r;
+        hipExtLaunchKernelGGL(hash_var_kernel<kHvKeys, DT>, dim3(p.total_sc), dim3(kHvBlock), hv_lds_bytes<kHvKeys>(),
+                              st, ev ? ev[0] : nullptr, nullptr, 0, aa, keys, hp, p.total_sc, ft);
+        ADL_HIP_TRY(hipGetLastError());
+        // the repeated-hash table pays for 16-byte keys only (configs[2]'s keys
+        // repeat few pairs: pass B 64 -> 70 us with it)
+        BuildArgs av = aa;
+        av.dd_log2 = 0;
+        rc = bin16(SrcH{hp, p.a.C}, av, true);
+      }
+    }
+    if (rc < 0)
+      rc = p.a.k == 6 ? go(adl_host::lds_limit<bloom_bin_kernel<B, 6, 6, Keys, DT>>, bloom_bin_kernel<B, 6, 6, Keys, DT>)
+                      : go(adl_host::lds_limit<bloom_bin_kernel<B, 0, kKptMax, Keys, DT>>,
+                           bloom_bin_kernel<B, 0, kKptMax, Keys, DT>);
     if (rc) return rc;
   }
   BuildArgs ab = aa;
-  ab.hot = hot_used;
   ab.claim = claim_used;
   t_last_claim = claim_used != 0;
-  if (!p.total_chunks) ab.dyn_tiles = 0;  // no pass A ran to reset the queue
   auto go_b = [&](auto lim, auto kern) -> int {
     if (int rc = lim()) return rc;
     hipExtLaunchKernelGGL(kern, dim3(p.grid_b), dim3(kBlockB), p.lds_b, st, ev ? ev[2] : nullptr,
                           ev ? ev[3] : nullptr, 0, ab, (const uint32_t *)pos_ws, (const uint32_t *)tab_ws,
-                          d_bitmaps, p.total_tiles, queue, ft);
+                          d_bitmaps, p.total_tiles, scr, ft);
     ADL_HIP_TRY(hipGetLastError());
     return ADL_OK;
   };
-  if (ab.hot) return go_b(adl_host::lds_limit<bloom_tile_kernel<8, DT, true>>, bloom_tile_kernel<8, DT, true>);
-  if (p.occ_b == 2) {
-    if (p.depth <= 4)
-      return go_b(adl_host::lds_limit<bloom_tile_kernel<4, DT, false, 2>>, bloom_tile_kernel<4, DT, false, 2>);
-    if (p.depth <= 6)
-      return go_b(adl_host::lds_limit<bloom_tile_kernel<6, DT, false, 2>>, bloom_tile_kernel<6, DT, false, 2>);
-    return go_b(adl_host::lds_limit<bloom_tile_kernel<8, DT, false, 2>>, bloom_tile_kernel<8, DT, false, 2>);
-  }
-  if (p.depth <= 4) return go_b(adl_host::lds_limit<bloom_tile_kernel<4, DT>>, bloom_tile_kernel<4, DT>);
-  if (p.depth <= 6) return go_b(adl_host::lds_limit<bloom_tile_kernel<6, DT>>, bloom_tile_kernel<6, DT>);
-  if (p.depth <= 8) return go_b(adl_host::lds_limit<bloom_tile_kernel<8, DT>>, bloom_tile_kernel<8, DT>);
-  return go_b(adl_host::lds_limit<bloom_tile_kernel<12, DT>>, bloom_tile_kernel<12, DT>);
+  if (p.occ_b == 2 && dyn_b)
+    return go_b(adl_host::lds_limit<bloom_tile_kernel<4, DT, 2, true>>, bloom_tile_kernel<4, DT, 2, true>);
+  if (dyn_b && p.occ_b == 1)
+    return go_b(adl_host::lds_limit<bloom_tile_kernel<kDepthB, DT, 1, true>>, bloom_tile_kernel<kDepthB, DT, 1, true>);
+  if (p.occ_b == 2)
+    return go_b(adl_host::lds_limit<bloom_tile_kernel<4, DT, 2>>, bloom_tile_kernel<4, DT, 2>);
+  return go_b(adl_host::lds_limit<bloom_tile_kernel<kDepthB, DT>>, bloom_tile_kernel<kDepthB, DT>);
 }
 
 template <class Keys>
@@ -1934,108 +1673,14 @@ int launch_binned(const Plan &p, Keys keys, uint8_t *d_bitmaps, void *ws, hipStr
   return p.dt ? launch_binned_dt<true>(p, keys, d_bitmaps, ws, st) : launch_binned_dt<false>(p, keys, d_bitmaps, ws, st);
 }
 
-template <class Keys>
-int launch_atomic(const Plan &p, Keys keys, uint8_t *d_bitmaps, hipStream_t st) {
-  for (const FilterDesc &d : p.f) {
-    const uint64_t n16 = d.alloc_bytes / 16;
-    hipLaunchKernelGGL(zero_kernel, dim3((uint32_t)std::min<uint64_t>((n16 + 255) / 256, 4096)), dim3(256), 0,
-                       st, reinterpret_cast<uint4 *>(d_bitmaps + d.bitmap_off), n16);
-    ADL_HIP_TRY(hipGetLastError());
-    if (d.n == 0) continue;
-    Keys kf = keys;
-    const uint64_t blocks = std::min<uint64_t>((d.n + 255) / 256, 256 * 32);
-    // key_begin offsets are applied through a shifted view
-    hipLaunchKernelGGL(bloom_atomic_kernel<Keys>, dim3((uint32_t)blocks), dim3(256), 0, st,
-                       shift_keys(kf, d.key_begin), (uint64_t)d.n, p.a.k, d.mod,
-                       reinterpret_cast<uint32_t *>(d_bitmaps + d.bitmap_off));
-    ADL_HIP_TRY(hipGetLastError());
-  }
-  return ADL_OK;
-}
-
-// The var-len hashing pass for the bucketed build (bloom_bucket.hip): (h1, h2)
-// of filter f's keys at pairs[key_begin[f] - key_begin[0] + ...], each run of
-// hv_keys keys in its length-sorted order (the bitmap is an OR, so the order
-// inside a filter's range does not matter).  hash_var_kernel unchanged: a
-// plan with C = 1 whose chunk_base is the filter's pair offset.  Past
-// kMaxFilters filters its descriptors and run map go to `scratch`
-// (adl_bk::var_layout).  ev0: the profiled pass-A interval opens here.
-int hash_pairs_var(KeysVar keys, const uint64_t *key_begin, uint32_t nf, uint2 *pairs, uint8_t *scratch,
-                   hipStream_t st, hipEvent_t ev0) {
-  static_assert(sizeof(FilterDesc) <= 128, "adl_bk::make_plan reserves 128 B per filter for this table");
-  BuildArgs a;
-  memset(&a, 0, sizeof(a));
-  a.nf = nf;
-  a.C = 1;
-  const uint32_t hk = env_u32("ADL_BLOOM_HV_KEYS", 512);
-  a.hv_keys = hk <= 256 ? 256 : hk <= 512 ? 512 : hk <= 1024 ? 1024 : 2048;
-#ifdef ADL_BLOOM_STAMPS
-  a.exp = env_u32("ADL_BLOOM_EXP", 0);
-#endif
-  std::vector<FilterDesc> fd(nf);
-  uint32_t sc = 0;
-  for (uint32_t f = 0; f < nf; ++f) {
-    FilterDesc &d = fd[f];
-    d = FilterDesc{};
-    d.key_begin = key_begin[f];
-    d.n = (uint32_t)(key_begin[f + 1] - key_begin[f]);
-    d.chunk_base = (uint32_t)(key_begin[f] - key_begin[0]);
-    d.sc_base = sc;
-    sc += (d.n + a.hv_keys - 1) / a.hv_keys;
-  }
-  if (!sc) {  // no keys: an empty hashing interval
-    if (ev0) ADL_HIP_TRY(hipEventRecord(ev0, st));
-    return ADL_OK;
-  }
-  const bool dt = nf > (uint32_t)kMaxFilters;
-  FilterTable ft{};
-  if (dt) {
-    FilterDesc *d_fd = reinterpret_cast<FilterDesc *>(scratch);
-    uint32_t *sc_f = reinterpret_cast<uint32_t *>(scratch + adl_host::round_up(nf * sizeof(FilterDesc), 256));
-    if (int rc = adl_host::t_upload.upload(d_fd, fd.data(), nf * sizeof(FilterDesc), st)) return rc;
-    // chunks = tiles = 0: only the run map is filled
-    hipLaunchKernelGGL(fill_maps_kernel, dim3(nf), dim3(256), 0, st, d_fd, sc_f, sc_f, sc_f, a.hv_keys);
-    ADL_HIP_TRY(hipGetLastError());
-    ft.fd = (cptr<FilterDesc>)d_fd;
-    ft.sc_f = (cptr<uint32_t>)sc_f;
-  } else {
-    std::copy(fd.begin(), fd.end(), a.f);
-  }
-  auto go = [&](auto lim, auto kern, size_t lds) -> int {
-    if (int rc = lim()) return rc;
-    hipExtLaunchKernelGGL(kern, dim3(sc), dim3(kHvBlock), lds, st, ev0, nullptr, 0, a, keys, pairs, sc, ft);
-    ADL_HIP_TRY(hipGetLastError());
-    return ADL_OK;
-  };
-#define ADL_HV(S)                                                                                          \
-  (dt ? go(adl_host::lds_limit<hash_var_kernel<S, true>>, hash_var_kernel<S, true>, hv_lds_bytes<S>())   \
-      : go(adl_host::lds_limit<hash_var_kernel<S, false>>, hash_var_kernel<S, false>, hv_lds_bytes<S>()))
-  const int rc = a.hv_keys == 256 ? ADL_HV(256) : a.hv_keys == 512 ? ADL_HV(512) : a.hv_keys == 1024 ? ADL_HV(1024)
-                                                                                                   : ADL_HV(2048);
-#undef ADL_HV
-  return rc;
-}
-
 }  // namespace
 
 namespace {
 // Runs the filters through the plan/launch pair: all in one launch pair (a
-// compaction's tables), split only where the u32 position indices of one
-// launch's workspace would overflow (groups of at most 2^31 / k keys).
-// ADL_BLOOM_GROUP_KEYS (tuning): a smaller cap, so a compaction's tables go
-// in several launch pairs (groups whose positions fit the Infinity Cache).
-uint64_t group_keys_max(int32_t bpk) {
-  const uint64_t cap = (1ull << 31) / (uint64_t)adl_host::num_probes(bpk);
-  if (const char *e = getenv("ADL_BLOOM_GROUP_KEYS")) {
-    const uint64_t v = strtoull(e, nullptr, 10);
-    if (v > 0) return std::min(cap, v);
-  }
-  return cap;
-}
-
-// whether this thread's last group went through the bucketed build (for
-// adl_bloom_build_positions, which reads that build's tables)
-thread_local bool t_last_bk = false;
+// compaction's tables; smaller launch groups measured slower), split only
+// where the u32 position indices of one launch's workspace would overflow
+// (groups of at most 2^31 / k keys).
+uint64_t group_keys_max(int32_t bpk) { return (1ull << 31) / (uint64_t)adl_host::num_probes(bpk); }
 
 int build_groups(const uint8_t *d_keys, const uint64_t *d_offsets, uint32_t key_stride,
                  const uint64_t *key_begin, uint32_t num_filters, int32_t bpk, uint8_t *d_bitmaps,
@@ -2045,7 +1690,6 @@ int build_groups(const uint8_t *d_keys, const uint64_t *d_offsets, uint32_t key_
   if (!d_keys && key_begin[num_filters] > key_begin[0]) return ADL_ERR_INVALID_ARG;
   if (!d_offsets && key_stride == 0 && key_begin[num_filters] > key_begin[0]) return ADL_ERR_INVALID_ARG;
   if (bpk < 0) return ADL_ERR_INVALID_ARG;
-  const bool atomic = use_atomic_path();
   const uint64_t gmax = group_keys_max(bpk);
   std::vector<uint64_t> counts;
   for (uint32_t g = 0; g < num_filters;) {
@@ -2060,52 +1704,6 @@ int build_groups(const uint8_t *d_keys, const uint64_t *d_offsets, uint32_t key_
       keys_in += c;
     }
     const uint32_t nf = e - g;
-    // 16-byte keys: the bucketed build (bloom_bucket.hip) when it takes the group
-    if (!atomic && !d_offsets && key_stride == 16 && (reinterpret_cast<uintptr_t>(d_keys) % 16) == 0 &&
-        !(flags & ADL_BLOOM_SKIP_ADJACENT_DUPLICATES) && adl_host::env_on("ADL_BLOOM_BK", false) &&
-        adl_bk::workspace_bytes(counts.data(), nf, bpk)) {
-      uint8_t *wsa = nullptr;
-      uint64_t wsb = 0;
-      if (d_workspace) {
-        wsa = reinterpret_cast<uint8_t *>(adl_host::round_up(reinterpret_cast<uintptr_t>(d_workspace), 256));
-        const uint64_t skip = (uint64_t)(wsa - static_cast<uint8_t *>(d_workspace));
-        wsb = workspace_bytes > skip ? workspace_bytes - skip : 0;
-      }
-      const int rc = adl_bk::build16(reinterpret_cast<const uint4 *>(d_keys), key_begin + g, nf, bpk, d_bitmaps,
-                                     bitmap_off + g, wsa, wsb, st, prof_slot());
-      if (rc) return rc;
-      t_last_bk = true;
-      g = e;
-      continue;
-    }
-    // variable-length keys (16-byte-aligned buffer): the hashing pass into
-    // (h1, h2) pairs, then the bucketed build over the pairs
-    if (!atomic && d_offsets && (reinterpret_cast<uintptr_t>(d_keys) % 16) == 0 &&
-        !(flags & ADL_BLOOM_SKIP_ADJACENT_DUPLICATES) && adl_host::env_on("ADL_BLOOM_BK", false) &&
-        adl_host::env_on("ADL_BLOOM_VAR_HASH", true) && adl_bk::workspace_bytes(counts.data(), nf, bpk)) {
-      uint8_t *wsa = nullptr;
-      uint64_t wsb = 0, pair_off = 0, scratch_off = 0;
-      if (d_workspace) {
-        wsa = reinterpret_cast<uint8_t *>(adl_host::round_up(reinterpret_cast<uintptr_t>(d_workspace), 256));
-        const uint64_t skip = (uint64_t)(wsa - static_cast<uint8_t *>(d_workspace));
-        wsb = workspace_bytes > skip ? workspace_bytes - skip : 0;
-      }
-      if (!wsa || wsb < adl_bk::workspace_bytes(counts.data(), nf, bpk)) return ADL_ERR_WORKSPACE;
-      if (int rc = adl_bk::var_layout(counts.data(), nf, bpk, &pair_off, &scratch_off)) return rc;
-      uint2 *pairs = reinterpret_cast<uint2 *>(wsa + pair_off);
-      hipEvent_t *ev = prof_slot();
-      if (int rc = hash_pairs_var(KeysVar{d_keys, d_offsets}, key_begin + g, nf, pairs, wsa + scratch_off, st,
-                                  ev ? ev[0] : nullptr))
-        return rc;
-      hipEvent_t evb[4] = {nullptr, ev ? ev[1] : nullptr, ev ? ev[2] : nullptr, ev ? ev[3] : nullptr};
-      if (int rc = adl_bk::build_pairs(pairs, key_begin + g, nf, bpk, d_bitmaps, bitmap_off + g, wsa, wsb, st,
-                                       ev ? evb : nullptr))
-        return rc;
-      t_last_bk = true;
-      g = e;
-      continue;
-    }
-    t_last_bk = false;
     Plan p;
     int rc = make_plan(counts.data(), nf, bpk, p);
     if (rc) return rc;
@@ -2116,21 +1714,18 @@ int build_groups(const uint8_t *d_keys, const uint64_t *d_offsets, uint32_t key_
       p.f[f].bitmap_off = bitmap_off[g + f];
       if (!p.dt) p.a.f[f] = p.f[f];
     }
-    if (!atomic && (!d_workspace || workspace_bytes < p.ws_bytes)) return ADL_ERR_WORKSPACE;
-    void *ws = d_workspace;
-    if (ws) ws = reinterpret_cast<void *>(adl_host::round_up(reinterpret_cast<uintptr_t>(ws), 256));
+    if (!d_workspace || workspace_bytes < p.ws_bytes) return ADL_ERR_WORKSPACE;
+    void *ws = reinterpret_cast<void *>(adl_host::round_up(reinterpret_cast<uintptr_t>(d_workspace), 256));
     if (d_offsets) {
       KeysVar keys{d_keys, d_offsets};
       // staging loads (pass A's windows and the hashing pass) read whole aligned
       // 16-byte blocks: only of a 16-byte-aligned key buffer
-      if (reinterpret_cast<uintptr_t>(d_keys) % 16) p.a.stage_keys = p.a.var_hash = 0;
-      rc = atomic ? launch_atomic(p, keys, d_bitmaps, st) : launch_binned(p, keys, d_bitmaps, ws, st);
+      if (reinterpret_cast<uintptr_t>(d_keys) % 16) p.a.stage_keys = 0;
+      rc = launch_binned(p, keys, d_bitmaps, ws, st);
     } else if (key_stride == 16 && (reinterpret_cast<uintptr_t>(d_keys) % 16) == 0) {
-      Keys16 keys{reinterpret_cast<const uint4 *>(d_keys)};
-      rc = atomic ? launch_atomic(p, keys, d_bitmaps, st) : launch_binned(p, keys, d_bitmaps, ws, st);
+      rc = launch_binned(p, Keys16{reinterpret_cast<const uint4 *>(d_keys)}, d_bitmaps, ws, st);
     } else {
-      KeysStride keys{d_keys, key_stride};
-      rc = atomic ? launch_atomic(p, keys, d_bitmaps, st) : launch_binned(p, keys, d_bitmaps, ws, st);
+      rc = launch_binned(p, KeysStride{d_keys, key_stride}, d_bitmaps, ws, st);
     }
     if (rc) return rc;
     g = e;
@@ -2163,15 +1758,18 @@ int adl_bloom_test_fault(int site, int64_t arg) {
   return ADL_OK;
 }
 
+int adl_bloom_reload_knobs(void) {
+  adl_host::reload_knobs();
+  return ADL_OK;
+}
+
 #ifdef ADL_BLOOM_STAMPS
 // Diagnostics build only: copies g_stamps ([pass][workgroup][phase] cycles).
-// Past those, the bucketed build's [2][2048][8] (bloom_bucket.hip).
 int adl_bloom_debug_stamps(uint64_t *out, uint64_t n) {
   constexpr uint64_t kOwn = 3 * 2048 * 8;
   const uint64_t bytes = std::min<uint64_t>(n, kOwn) * 8;
   ADL_HIP_TRY(hipDeviceSynchronize());
   ADL_HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), bytes, 0, hipMemcpyDeviceToHost));
-  if (n > kOwn) return adl_bk::debug_stamps(out + kOwn, n - kOwn);
   return ADL_OK;
 }
 #endif
@@ -2218,10 +1816,6 @@ uint64_t adl_bloom_build_workspace_bytes(const uint64_t *key_counts, uint32_t nu
     Plan p;
     if (make_plan(key_counts + g, e - g, bits_per_key, p)) return 0;
     ws = std::max(ws, p.ws_bytes);
-    // the bucketed build (ADL_BLOOM_BK=1, measured slower overall: DESIGN.md
-    // §5) needs its own, larger workspace; sized for only when selected
-    if (adl_host::env_on("ADL_BLOOM_BK", false))
-      ws = std::max(ws, adl_bk::workspace_bytes(key_counts + g, e - g, bits_per_key));
     g = e;
   }
   return ws;
@@ -2246,8 +1840,6 @@ int adl_bloom_build_positions(const uint64_t *key_counts, uint32_t num_filters, 
       g0 = e;
     }
     hipStream_t st = adl_host::sync_stream(stream);
-    const void *wsa = reinterpret_cast<const void *>(adl_host::round_up(reinterpret_cast<uintptr_t>(d_workspace), 256));
-    if (t_last_bk) return adl_bk::positions(key_counts + g, num_filters - g, bits_per_key, wsa, positions, st);
     Plan p;
     if (int rc = make_plan(key_counts + g, num_filters - g, bits_per_key, p)) return rc;
     const uint32_t *tab = reinterpret_cast<const uint32_t *>(

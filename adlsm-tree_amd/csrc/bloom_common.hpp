@@ -189,6 +189,58 @@ __device__ __forceinline__ uint32_t block_excl_scan_array_1b(uint32_t *a, uint32
 
 namespace adl_host {
 
+// Tuning and test switches, read from the environment once per
+// process.  adl_bloom_reload_knobs() reads them again (tests, between calls:
+// no call of the library may be running).
+struct Knobs {
+  uint32_t tile_log2 = 0;         // ADL_BLOOM_TILE_LOG2: pass-B tile bits (10..20; 0: the plan's choice)
+  uint32_t claim = 3;             // ADL_BLOOM_CLAIM: 0 off, 1 wherever the share test passes, 2 forced, 3 auto
+  uint32_t claim_cap = 0;         // ADL_BLOOM_CLAIM_CAP: claim region cap, percent of k*C (0: the LDS left)
+  bool hash_dedup = true;         // ADL_BLOOM_HASH_DEDUP: pass A skips repeated hash pairs
+  bool spin = true;               // ADL_BLOOM_SPIN: small cache probes watch their mapped answers
+  bool probe_server = true;       // ADL_BLOOM_PROBE_SERVER: cache batches of <= 8 queries go to the server
+  uint64_t server_idle_us = 2000;   // ADL_BLOOM_SERVER_IDLE_US
+  uint64_t server_life_us = 20000;  // ADL_BLOOM_SERVER_LIFE_US
+  uint64_t pipe_mb = 128;         // ADL_BLOOM_PIPE_MB: keys per group of the pipelined host build
+  bool debug = false;             // ADL_BLOOM_DEBUG: the plan and failing HIP calls to stderr
+  uint32_t exp = 0, pb_exp = 0;   // ADL_BLOOM_EXP / ADL_PB_EXP: diagnostics build (make stamps) only
+
+  void load() {
+    auto u64 = [](const char *name, uint64_t dflt) -> uint64_t {
+      const char *e = getenv(name);
+      return e && *e ? strtoull(e, nullptr, 10) : dflt;
+    };
+    *this = Knobs{};
+    tile_log2 = (uint32_t)u64("ADL_BLOOM_TILE_LOG2", 0);
+    claim = (uint32_t)u64("ADL_BLOOM_CLAIM", 3);
+    claim_cap = (uint32_t)u64("ADL_BLOOM_CLAIM_CAP", 0);
+    hash_dedup = u64("ADL_BLOOM_HASH_DEDUP", 1) != 0;
+    spin = u64("ADL_BLOOM_SPIN", 1) != 0;
+    probe_server = u64("ADL_BLOOM_PROBE_SERVER", 1) != 0;
+    server_idle_us = u64("ADL_BLOOM_SERVER_IDLE_US", 2000);
+    server_life_us = u64("ADL_BLOOM_SERVER_LIFE_US", 20000);
+    pipe_mb = u64("ADL_BLOOM_PIPE_MB", 128);
+    debug = u64("ADL_BLOOM_DEBUG", 0) != 0;
+#ifdef ADL_BLOOM_STAMPS
+    exp = (uint32_t)u64("ADL_BLOOM_EXP", 0);
+    pb_exp = (uint32_t)u64("ADL_PB_EXP", 0);
+#endif
+  }
+};
+
+inline Knobs g_knobs;
+inline std::once_flag g_knobs_once;
+
+inline const Knobs &knobs() {
+  std::call_once(g_knobs_once, [] { g_knobs.load(); });
+  return g_knobs;
+}
+
+inline void reload_knobs() {
+  (void)knobs();
+  g_knobs.load();
+}
+
 // Host-side magic numbers for adl_dev::fastmod (see murmur3_device.hpp).
 inline adl_dev::FastMod make_fastmod(uint32_t m) {
   adl_dev::FastMod f{};
@@ -297,12 +349,6 @@ struct MappedStage {
 };
 
 inline thread_local MappedStage t_mapped;
-
-// A boolean environment switch (read per call, so tests can flip it).
-inline bool env_on(const char *name, bool dflt) {
-  const char *e = getenv(name);
-  return e ? atoi(e) != 0 : dflt;
-}
 
 // The stream a synchronous host-pointer entry point runs on: the caller's, or
 // for stream == NULL a non-blocking stream of the calling thread (created on

@@ -113,9 +113,10 @@ struct Group {
 
 }  // namespace
 
-extern "C" int adl_bloom_build_segmented(const uint8_t *h_keys, const uint64_t *h_offsets, uint32_t key_stride,
-                                         const uint64_t *key_begin, uint32_t num_filters, int32_t bits_per_key,
-                                         uint8_t *h_bitmaps, const uint64_t *h_bitmap_off, void *stream) {
+namespace {
+int segmented_host(const uint8_t *h_keys, const uint64_t *h_offsets, uint32_t key_stride,
+                   const uint64_t *key_begin, uint32_t num_filters, int32_t bits_per_key,
+                   uint8_t *h_bitmaps, const uint64_t *h_bitmap_off, uint32_t flags, void *stream) {
   try {
     if (!key_begin || !h_bitmap_off || !h_bitmaps || num_filters == 0) return ADL_ERR_INVALID_ARG;
     if (bits_per_key < 0) return ADL_ERR_INVALID_ARG;
@@ -128,8 +129,8 @@ extern "C" int adl_bloom_build_segmented(const uint8_t *h_keys, const uint64_t *
     auto key_byte = [&](uint64_t k) -> uint64_t { return h_offsets ? h_offsets[k] : k * (uint64_t)key_stride; };
 
     // groups of consecutive filters
-    const char *mb_env = getenv("ADL_BLOOM_PIPE_MB");
-    const uint64_t group_bytes = mb_env && atoll(mb_env) > 0 ? (uint64_t)atoll(mb_env) << 20 : kGroupKeyBytes;
+    const uint64_t pipe_mb = adl_host::knobs().pipe_mb;
+    const uint64_t group_bytes = pipe_mb > 0 ? pipe_mb << 20 : kGroupKeyBytes;
     std::vector<Group> groups;
     uint64_t max_in = 0, max_out = 0, max_ws = 0;
     for (uint32_t f0 = 0; f0 < num_filters;) {
@@ -240,9 +241,9 @@ extern "C" int adl_bloom_build_segmented(const uint8_t *h_keys, const uint64_t *
       const uint8_t *d_keys = h_offsets ? P.d_in[b] - g.b0 : P.d_in[b];
       const uint64_t *d_offs = h_offsets ? reinterpret_cast<const uint64_t *>(P.d_in[b] + kb_al) : nullptr;
       if ((long)gi == fault_group) return ADL_ERR_DEVICE;
-      if (int rc = adl_bloom_build_segmented_device(d_keys, d_offs, key_stride, local_kb.data(), g.f1 - g.f0,
-                                                    bits_per_key, P.d_out[b], dev_off.data(), P.d_ws, P.ws_cap,
-                                                    comp))
+      if (int rc = adl_bloom_build_segmented_device_ex(d_keys, d_offs, key_stride, local_kb.data(), g.f1 - g.f0,
+                                                       bits_per_key, P.d_out[b], dev_off.data(), flags, P.d_ws,
+                                                       P.ws_cap, comp))
         return rc;
       ADL_HIP_TRY(hipEventRecord(P.ev_built[b], comp));
 
@@ -285,4 +286,21 @@ extern "C" int adl_bloom_build_segmented(const uint8_t *h_keys, const uint64_t *
   } catch (...) {
     return ADL_ERR_DEVICE;
   }
+}
+}  // namespace
+
+extern "C" int adl_bloom_build_segmented(const uint8_t *h_keys, const uint64_t *h_offsets, uint32_t key_stride,
+                                         const uint64_t *key_begin, uint32_t num_filters, int32_t bits_per_key,
+                                         uint8_t *h_bitmaps, const uint64_t *h_bitmap_off, void *stream) {
+  return segmented_host(h_keys, h_offsets, key_stride, key_begin, num_filters, bits_per_key, h_bitmaps,
+                        h_bitmap_off, 0, stream);
+}
+
+extern "C" int adl_bloom_build_segmented_ex(const uint8_t *h_keys, const uint64_t *h_offsets, uint32_t key_stride,
+                                            const uint64_t *key_begin, uint32_t num_filters, int32_t bits_per_key,
+                                            uint8_t *h_bitmaps, const uint64_t *h_bitmap_off, uint32_t flags,
+                                            void *stream) {
+  if (flags & ~(uint32_t)ADL_BLOOM_SKIP_ADJACENT_DUPLICATES) return ADL_ERR_INVALID_ARG;
+  return segmented_host(h_keys, h_offsets, key_stride, key_begin, num_filters, bits_per_key, h_bitmaps,
+                        h_bitmap_off, flags, stream);
 }

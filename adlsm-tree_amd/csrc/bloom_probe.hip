@@ -26,48 +26,31 @@ namespace {
 
 constexpr int kBlockP = 256;
 
-constexpr uint32_t kProbeFirst = 1;      // bitmap reads in the first round of a query (default)
-constexpr uint32_t kProbeGroup = 1;      // ... and in every later round (default)
-constexpr uint32_t kProbeGroupMax = 8;
 constexpr uint32_t kLdsFilters = 4096;   // per-filter divisor table kept in LDS up to this many
 
-// The k bitmap reads of one query, issued in rounds (`first`, then `rest` at
-// a time, both <= kProbeGroupMax) so independent random reads overlap while a
-// clear bit still ends the query early, like the reference's loop
-// (src/filter_block.cpp:54-59).  The answer does not depend on the grouping.
-struct ProbeGroups {
-  uint32_t first, rest;
-};
-
+// The k bitmap reads of one query, one at a time with the reference's stop at
+// the first clear bit (src/filter_block.cpp:54-59).  Issuing 2-8 reads per
+// round (so they overlap) measured slower: the probe is bound by random HBM
+// reads, so the fewest reads win.
 __device__ __forceinline__ uint8_t probe_bits(const uint8_t *__restrict__ bm, uint32_t h1, uint32_t h2,
-                                              uint32_t k, const FastMod &mod, ProbeGroups pg) {
-  uint32_t j = 0, group = pg.first;
-  while (j < k) {
-    uint32_t all = 1;
-#pragma unroll
-    for (uint32_t g = 0; g < kProbeGroupMax; ++g) {
-      if (g < group && j + g < k) {
-        const uint32_t p = fastmod(h1 + (j + g) * h2, mod);
-        all &= (uint32_t)(bm[p >> 3] >> (p & 7));
-      }
-    }
-    if (!(all & 1u)) return 0;
-    j += group;
-    group = pg.rest;
+                                              uint32_t k, const FastMod &mod) {
+  for (uint32_t j = 0; j < k; ++j) {
+    const uint32_t p = fastmod(h1 + j * h2, mod);
+    if (!((bm[p >> 3] >> (p & 7)) & 1u)) return 0;
   }
   return 1;
 }
 
 template <class Keys>
 __global__ __launch_bounds__(kBlockP) void bloom_probe_kernel(Keys keys, uint64_t n, uint32_t k,
-                                                              FastMod mod, ProbeGroups pg,
+                                                              FastMod mod,
                                                               const uint8_t *__restrict__ bitmap,
                                                               uint8_t *__restrict__ out) {
   for (uint64_t i = blockIdx.x * (uint64_t)kBlockP + threadIdx.x; i < n;
        i += (uint64_t)gridDim.x * kBlockP) {
     uint32_t h1, h2;
     keys.hash(i, h1, h2);
-    out[i] = probe_bits(bitmap, h1, h2, k, mod, pg);
+    out[i] = probe_bits(bitmap, h1, h2, k, mod);
   }
 }
 
@@ -81,7 +64,7 @@ struct ModLds {
 
 template <class Keys>
 __global__ __launch_bounds__(kBlockP) void bloom_probe_multi_kernel(
-    Keys keys, uint64_t n, uint32_t k, ProbeGroups pg, const uint32_t *__restrict__ fid, uint32_t uniform_f,
+    Keys keys, uint64_t n, uint32_t k, const uint32_t *__restrict__ fid, uint32_t uniform_f,
     uint32_t nf, const uint8_t *__restrict__ bitmaps, const uint64_t *__restrict__ boff,
     const uint64_t *__restrict__ bend, uint8_t *__restrict__ out) {
   // filter f = bitmaps[boff[f], bend[f]), or [boff[f], boff[f+1]) when bend is null
@@ -117,7 +100,7 @@ __global__ __launch_bounds__(kBlockP) void bloom_probe_multi_kernel(
         }
         uint32_t h1, h2;
         keys.hash(i, h1, h2);
-        hit = probe_bits(bitmaps + b0, h1, h2, k, mod, pg);
+        hit = probe_bits(bitmaps + b0, h1, h2, k, mod);
       }
     }
     out[i] = hit;
@@ -245,17 +228,6 @@ inline uint32_t grid_for(uint64_t n, int block, uint32_t blocks_per_cu = 64) {
       1, std::min<uint64_t>((n + block - 1) / block, (uint64_t)adl_host::device_cus() * blocks_per_cu));
 }
 
-// ADL_BLOOM_PROBE_GROUPS="first,rest" (default "1,1": measured best, the probe is bound by random HBM reads, so the fewest reads win): bitmap reads per round.
-ProbeGroups probe_groups() {
-  ProbeGroups pg{kProbeFirst, kProbeGroup};
-  if (const char *e = getenv("ADL_BLOOM_PROBE_GROUPS")) {
-    unsigned f = 0, r = 0;
-    if (sscanf(e, "%u,%u", &f, &r) == 2 && f >= 1 && r >= 1 && f <= kProbeGroupMax && r <= kProbeGroupMax)
-      pg = ProbeGroups{f, r};
-  }
-  return pg;
-}
-
 template <class F>
 int dispatch_keys(const uint8_t *d_keys, const uint64_t *d_offsets, uint32_t key_stride, F &&fn) {
   if (d_offsets) return fn(KeysVar{d_keys, d_offsets});
@@ -281,7 +253,7 @@ int adl_bloom_probe_device(const uint8_t *d_keys, const uint64_t *d_offsets, uin
   hipStream_t st = (hipStream_t)stream;
   return dispatch_keys(d_keys, d_offsets, key_stride, [&](auto keys) -> int {
     hipLaunchKernelGGL(bloom_probe_kernel<decltype(keys)>, dim3(grid_for(n, kBlockP)), dim3(kBlockP), 0,
-                       st, keys, n, k, mod, probe_groups(), d_bitmap, d_out);
+                       st, keys, n, k, mod, d_bitmap, d_out);
     ADL_HIP_TRY(hipGetLastError());
     return ADL_OK;
   });
@@ -303,7 +275,7 @@ int probe_multi(const uint8_t *d_keys, const uint64_t *d_offsets, uint64_t n, ui
     const size_t lds = num_filters <= kLdsFilters ? (size_t)num_filters * sizeof(ModLds) : 0;
     // `done` rides on the dispatch packet itself (no marker packet after it)
     hipExtLaunchKernelGGL(bloom_probe_multi_kernel<decltype(keys)>, dim3(grid_for(n, kBlockP, 8)),
-                          dim3(kBlockP), lds, st, nullptr, done, 0, keys, n, k, probe_groups(), d_filter_id,
+                          dim3(kBlockP), lds, st, nullptr, done, 0, keys, n, k, d_filter_id,
                           uniform_f, num_filters, d_bitmaps, d_bitmap_off, d_bitmap_end, d_out);
     ADL_HIP_TRY(hipGetLastError());
     return ADL_OK;

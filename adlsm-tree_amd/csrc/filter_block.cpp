@@ -7,6 +7,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <map>
@@ -18,6 +19,11 @@
 namespace adl {
 
 namespace {
+
+/* FilterBlockWriter::Final skips adjacent duplicate keys on the device when at
+ * least Num/Den of its keys are such duplicates (the generic pass A it then
+ * runs costs more than the fast paths on keys without them). */
+constexpr uint64_t kSkipDuplicatesNum = 1, kSkipDuplicatesDen = 3;
 
 /* Decode32 (reference src/encode.cpp:6): native-endian unaligned int32 load. */
 int Load32(const char *src) {
@@ -98,7 +104,7 @@ RC FilterAlgorithm::IsKeysExist(const KeyArena &keys, string_view bitmap, vector
 }
 
 RC FilterAlgorithm::Keys2Blocks(const KeyArena &keys, const vector<uint64_t> &key_begin, string &result,
-                                vector<uint64_t> &starts) {
+                                vector<uint64_t> &starts, bool /*adjacent_duplicates*/) {
   starts.clear();
   for (size_t f = 0; f + 1 < key_begin.size(); ++f) {
     starts.push_back(result.size());
@@ -111,9 +117,10 @@ RC FilterAlgorithm::Keys2Blocks(const KeyArena &keys, const vector<uint64_t> &ke
 }
 
 /* All filters of a block in one pipelined segmented build, each bitmap written
- * in place at the offset successive Keys2Block appends would give it. */
+ * in place at the offset successive Keys2Block appends would give it.  With
+ * many adjacent duplicates the build skips them (same bitmaps). */
 RC BloomFilter::Keys2Blocks(const KeyArena &keys, const vector<uint64_t> &key_begin, string &result,
-                            vector<uint64_t> &off) {
+                            vector<uint64_t> &off, bool adjacent_duplicates) {
   const size_t nf = key_begin.size() - 1;
   off.assign(nf, 0);
   if (nf == 0) return OK;
@@ -126,10 +133,10 @@ RC BloomFilter::Keys2Blocks(const KeyArena &keys, const vector<uint64_t> &key_be
     total += bytes;
   }
   result.resize(init_len + total);
-  const int st = adl_bloom_build_segmented(reinterpret_cast<const uint8_t *>(keys.bytes().data()),
-                                           keys.offsets().data(), 0, key_begin.data(), (uint32_t)nf,
-                                           bits_per_key_, reinterpret_cast<uint8_t *>(&result[0]), off.data(),
-                                           nullptr);
+  const int st = adl_bloom_build_segmented_ex(
+      reinterpret_cast<const uint8_t *>(keys.bytes().data()), keys.offsets().data(), 0, key_begin.data(),
+      (uint32_t)nf, bits_per_key_, reinterpret_cast<uint8_t *>(&result[0]), off.data(),
+      adjacent_duplicates ? ADL_BLOOM_SKIP_ADJACENT_DUPLICATES : 0u, nullptr);
   if (st != ADL_OK) {
     result.resize(init_len);
     return FromStatus(st);
@@ -181,13 +188,24 @@ FilterBlockWriter::FilterBlockWriter(unique_ptr<FilterAlgorithm> &&method)
 
 /* src/filter_block.cpp:72-75 */
 RC FilterBlockWriter::Update(string_view key) {
+  const size_t from = keys_.size();
   keys_.Add(key);
+  CountDuplicates(from);
   return OK;
 }
 
 RC FilterBlockWriter::UpdateBatch(const char *base, const uint64_t *off, size_t n, size_t trim) {
+  const size_t from = keys_.size();
   keys_.AddTrimmed(base, off, n, trim);
+  CountDuplicates(from);
   return OK;
+}
+
+/* keys [from, size) against their predecessors in the same filter: a user
+ * key's versions arrive in a row (memtable order, src/keys.cpp:61-74) */
+void FilterBlockWriter::CountDuplicates(size_t from) {
+  for (size_t i = std::max<size_t>(from, bounds_.back() + 1); i < keys_.size(); ++i)
+    dups_ += keys_.key(i) == keys_.key(i - 1);
 }
 
 /* src/filter_block.cpp:104-109 -- closes the current filter; its bitmap is
@@ -203,9 +221,13 @@ RC FilterBlockWriter::Keys2Block() {
 RC FilterBlockWriter::Final(string &result) {
   if (keys_.size() > bounds_.back()) Keys2Block();
   vector<uint64_t> offsets;
-  const RC rc = method_->Keys2Blocks(keys_, bounds_, buffer_, offsets);
+  // Skipping duplicates runs the generic pass A (keys in their order), which
+  // only pays when they are frequent (adjacent duplicates).
+  const bool skip = dups_ * kSkipDuplicatesDen >= keys_.size() * kSkipDuplicatesNum && dups_ > 0;
+  const RC rc = method_->Keys2Blocks(keys_, bounds_, buffer_, offsets, skip);
   keys_.Clear();
   bounds_.assign(1, 0);
+  dups_ = 0;
   if (rc != OK) {
     buffer_.clear();
     return rc;

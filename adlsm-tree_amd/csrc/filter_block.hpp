@@ -92,9 +92,11 @@ class FilterAlgorithm {
   /* Keys2Block for consecutive filters: filter f = keys [key_begin[f],
    * key_begin[f+1]); the bitmaps are appended to result back to back, as
    * successive Keys2Block calls would, filter f starting at starts[f].  The
-   * default loops over Keys2Block. */
+   * default loops over Keys2Block.  adjacent_duplicates: a hint that many keys
+   * equal their predecessor (versions of one user key in memtable order); the
+   * result is the same either way, an implementation may skip such keys. */
   virtual RC Keys2Blocks(const KeyArena &keys, const vector<uint64_t> &key_begin, string &result,
-                         vector<uint64_t> &starts);
+                         vector<uint64_t> &starts, bool adjacent_duplicates = false);
   /* out[i] = IsKeyExists(key i, bitmap); the default loops over IsKeyExists */
   virtual RC IsKeysExist(const KeyArena &keys, string_view bitmap, vector<uint8_t> &out);
   virtual ~FilterAlgorithm() = default;
@@ -109,7 +111,7 @@ class BloomFilter : public FilterAlgorithm {
   void FilterInfo(string &info) override;
   RC Keys2Block(const KeyArena &keys, string &result) override;
   RC Keys2Blocks(const KeyArena &keys, const vector<uint64_t> &key_begin, string &result,
-                 vector<uint64_t> &starts) override;
+                 vector<uint64_t> &starts, bool adjacent_duplicates = false) override;
   RC IsKeysExist(const KeyArena &keys, string_view bitmap, vector<uint8_t> &out) override;
   int bits_per_key() const { return bits_per_key_; }
   int num_probes() const { return k_; }
@@ -129,10 +131,14 @@ class FilterBlockWriter {
   RC UpdateBatch(const char *base, const uint64_t *off, size_t n, size_t trim);
   RC Final(string &result);
   RC Keys2Block();
+  /* keys added since the last Final that equal the previous key of their filter */
+  uint64_t adjacent_duplicates() const { return dups_; }
 
  private:
+  void CountDuplicates(size_t from);
   KeyArena keys_;              /* keys of every filter not yet built */
   vector<uint64_t> bounds_{0}; /* filter f = keys_ [bounds_[f], bounds_[f+1]) */
+  uint64_t dups_ = 0;          /* adjacent duplicates among keys_ (CountDuplicates) */
   string buffer_;
   unique_ptr<FilterAlgorithm> method_;
 };

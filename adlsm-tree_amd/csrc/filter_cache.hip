@@ -345,7 +345,7 @@ int adl_bloom_filter_cache_probe(adl_bloom_filter_cache *c, const char *const *o
     {
       const uint64_t kbytes = h_offsets ? h_offsets[n] - h_offsets[0] : n * (uint64_t)key_stride;
       adl_srv::Server *srv = nullptr;
-      if (adl_srv::eligible(n, kbytes) && adl_host::env_on("ADL_BLOOM_PROBE_SERVER", true)) {
+      if (adl_srv::eligible(n, kbytes) && adl_host::knobs().probe_server) {
         std::lock_guard<std::mutex> g(c->mu);
         if (!c->srv_tried) {
           c->srv_tried = true;
@@ -363,10 +363,14 @@ int adl_bloom_filter_cache_probe(adl_bloom_filter_cache *c, const char *const *o
         int rc = adl_srv::probe(srv, h_keys, h_offsets, key_stride, n, rng, (uint32_t)adl_host::num_probes(c->bpk),
                                 h_out);
         if (rc == ADL_OK && adl_host::g_test_faults.take(ADL_TEST_FAULT_CACHE_COMPLETION) >= 0) rc = ADL_ERR_DEVICE;
-        unpin_all();
-        if (rc) return rc;
-        if (h_uncached) *h_uncached = uncached;
-        return ADL_OK;
+        // kBusy: no answer in adl_srv::kTimeout (a healthy GPU with no room for
+        // the server's wave): probe by a launch below, the ranges still pinned
+        if (rc != adl_srv::kBusy) {
+          unpin_all();
+          if (rc) return rc;
+          if (h_uncached) *h_uncached = uncached;
+          return ADL_OK;
+        }
       }
     }
     // 2. without the lock: stage keys, offsets, table ids and the range table
@@ -395,7 +399,7 @@ int adl_bloom_filter_cache_probe(adl_bloom_filter_cache *c, const char *const *o
     // completion event has fired too, so a fault after the answers landed is
     // still this call's error.  Both waits fall back to the synchronize after
     // 2 ms (or with ADL_BLOOM_SPIN=0).
-    const bool spin = hbuf != sg.host && n <= 4096 && adl_host::env_on("ADL_BLOOM_SPIN", true);
+    const bool spin = hbuf != sg.host && n <= 4096 && adl_host::knobs().spin;
     if (rc == ADL_OK) {
       if (key_bytes) memcpy(hbuf, h_keys, key_bytes);
       if (off_bytes) memcpy(hbuf + o_offs, h_offsets, off_bytes);

@@ -112,33 +112,6 @@ __device__ __forceinline__ void hash16(uint4 raw, uint32_t &h1, uint32_t &h2) {
   h2 = fmix(b, 16u);
 }
 
-// Collapsed 16-byte keys.  The last block's rotate (src/murmur3_hash.cpp:5-9,
-// :36) of a negative state s is (s << 13) | (s >> 19, arithmetic) =
-// 0xFFFFF000 | s[30:19]: 12 bits survive.  When both seeds' states are
-// negative there and agree in bits 30..19, the key's two hashes are equal and
-// one of 4 096 values fixed by the algorithm alone (hot_h16); 25 % of random
-// keys do this (SplitMix64, 10 M keys: 2 515 004 of them, all 4 096 indices).
-// Such a key sets exactly the bits (j+1) * hot_h16(i) % m, j < k, whatever
-// its bytes, so a build needs each present index once, not each key.
-__device__ __forceinline__ uint32_t hot_h16(uint32_t i) { return fmix(mix_s(0x80000000u | (i << 19)), 16u); }
-
-// hash16 that also reports the collapse when `en`: hot = true, h1 = the index
-// i (h2 unspecified); otherwise (or !en) h1/h2 as hash16.
-__device__ __forceinline__ void hash16h(uint4 raw, uint32_t &h1, uint32_t &h2, bool &hot, bool en) {
-  const uint32_t w0 = quirk_word(raw.x), w1 = quirk_word(raw.y);
-  const uint32_t w2 = quirk_word(raw.z), w3 = quirk_word(raw.w);
-  uint32_t a = kSeed1, b = kSeed2;
-  mix_block2(a, b, w0);
-  mix_block2(a, b, w1);
-  mix_block2(a, b, w2);
-  const uint32_t kk = mix_k(w3);
-  const uint32_t sa = a ^ kk, sb = b ^ kk;
-  h1 = fmix(mix_s(sa), 16u);
-  h2 = fmix(mix_s(sb), 16u);
-  hot = en && (int32_t)(sa & sb) < 0 && ((sa ^ sb) & 0x7FF80000u) == 0;
-  if (hot) h1 = (sa >> 19) & 0xFFFu;
-}
-
 // Unaligned little-endian 32-bit read of 4 bytes (global or LDS generic pointer).
 __device__ __forceinline__ uint32_t load_u32_unaligned(const uint8_t *p) {
   uint32_t v;
@@ -223,42 +196,6 @@ __device__ __forceinline__ void hash_lds(const uint32_t *stage, uint32_t off, ui
   }
   ha = fmix(a, len);
   hb = fmix(b, len);
-}
-
-// One seed of a key staged in LDS (hash_lds with a single state): the
-// var-len hashing pass splits a run's longest keys between two waves, one
-// seed each.
-__device__ __forceinline__ uint32_t hash_lds1(const uint32_t *stage, uint32_t off, uint32_t len, uint32_t seed) {
-  uint32_t a = seed;
-  const uint32_t nblk = len >> 2, sh = off & 3u;
-  uint32_t wi = off >> 2;
-  uint32_t i = 0;
-  const uint2 *s2 = reinterpret_cast<const uint2 *>(stage);
-  const bool odd = (wi & 1u) != 0;
-  uint2 p0 = s2[wi >> 1];
-  uint32_t lo = odd ? p0.y : p0.x;
-  uint32_t pi = wi >> 1;
-  for (; i + 4 <= nblk; i += 4) {
-    const uint2 p1 = s2[pi + 1], p2 = s2[pi + 2];
-    const uint32_t w[4] = {odd ? p1.x : p0.y, odd ? p1.y : p1.x, odd ? p2.x : p1.y, odd ? p2.y : p2.x};
-#pragma unroll
-    for (int u = 0; u < 4; ++u) a = mix_block(a, quirk_word(__builtin_amdgcn_alignbyte(w[u], u ? w[u - 1] : lo, sh)));
-    lo = w[3];
-    p0 = p2;
-    pi += 2;
-    wi += 4;
-  }
-  for (; i < nblk; ++i) {
-    const uint32_t hi = stage[++wi];
-    a = mix_block(a, quirk_word(__builtin_amdgcn_alignbyte(hi, lo, sh)));
-    lo = hi;
-  }
-  const uint32_t rem = len & 3u;
-  if (rem) {
-    const uint32_t raw = __builtin_amdgcn_alignbyte(stage[wi + 1], lo, sh);
-    a ^= mix_tail_k(tail_word(raw, rem));
-  }
-  return fmix(a, len);
 }
 
 // h % m for a launch-constant divisor 2 <= m < 2^31 (Granlund-Montgomery

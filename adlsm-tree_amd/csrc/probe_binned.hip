@@ -61,7 +61,6 @@ constexpr uint32_t kSentinel = 0xFFFFFFFFu;
 constexpr uint16_t kNoSlot = 0xFFFF;            // a query that is answered 0 without probing
 constexpr uint32_t kLdsWords = 40960;           // 160 KiB
 constexpr uint64_t kMinBinned = 1ull << 20;     // below this the direct kernel wins
-constexpr uint32_t kSplit6 = 0;                 // k = 6: bits in the first of two rounds (0: one round)
 
 struct PFilter {
   uint32_t m, magic, shift, tiles;
@@ -281,77 +280,6 @@ __global__ __launch_bounds__(kBlk) void pb_starts_kernel(const uint32_t *__restr
   }
 }
 
-__global__ __launch_bounds__(256) void pb_rows_kernel(const uint32_t *__restrict__ hist, uint32_t nb, uint32_t F,
-                                                      PFilter *__restrict__ desc) {
-  __shared__ uint32_t red[256];
-  const uint32_t f = blockIdx.x;
-  uint32_t s = 0;
-  for (uint32_t b = threadIdx.x; b < nb; b += 256) s += hist[(uint64_t)b * (F + 1) + f];
-  red[threadIdx.x] = s;
-  __syncthreads();
-  for (uint32_t h = 128; h; h >>= 1) {
-    if (threadIdx.x < h) red[threadIdx.x] += red[threadIdx.x + h];
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) desc[f].cnt = red[0];
-}
-
-__device__ __forceinline__ uint64_t block_sum64(uint64_t v, uint64_t *red) {
-  const uint32_t lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
-  for (int o = kWave / 2; o; o >>= 1) v += __shfl_xor(v, o, kWave);
-  if (lane == 0) red[wave] = v;
-  __syncthreads();
-  uint64_t t = 0;
-  for (uint32_t w = 0; w < kBlk / kWave; ++w) t += red[w];
-  __syncthreads();
-  return t;
-}
-
-__global__ __launch_bounds__(kBlk) void pb_scan_kernel(const uint32_t *__restrict__ cnt_, uint32_t *__restrict__ start,
-                                                       uint32_t nb, uint32_t F, uint32_t C, uint64_t maxch,
-                                                       PFilter *__restrict__ desc, uint32_t *__restrict__ chunk_filter,
-                                                       uint32_t *__restrict__ scal) {
-  __shared__ uint64_t red[kBlk / kWave];
-  __shared__ uint32_t scratch[kBlk / kWave + 1];
-  const uint32_t f = blockIdx.x;
-  // sums over the filters before f: queries, chunks, table entries
-  uint64_t sq = 0, sc = 0, st = 0;
-  for (uint32_t g = threadIdx.x; g < f; g += kBlk) {
-    const uint32_t cg = desc[g].cnt, tg = desc[g].tiles;
-    const uint32_t nc = (cg + C - 1) / C;
-    sq += cg;
-    sc += nc;
-    st += (uint64_t)(tg + 1) * nc;
-  }
-  sq = block_sum64(sq, red);
-  sc = block_sum64(sc, red);
-  st = block_sum64(st, red);
-  const uint32_t cnt = desc[f].cnt;
-  const uint32_t nc = f < F ? (cnt + C - 1) / C : 0u;  // the out-of-range bucket has no chunks
-  if (threadIdx.x == 0) {
-    desc[f].qbase = (uint32_t)sq;
-    desc[f].chunk_base = (uint32_t)sc;
-    desc[f].nchunks = nc;
-    desc[f].table_base = st;
-    if (f == F) scal[1] = (uint32_t)sc;  // chunks over all filters
-  }
-  for (uint32_t j = threadIdx.x; j < nc; j += kBlk) chunk_filter[sc + j] = f;
-  if (f == F)
-    for (uint64_t j = sc + threadIdx.x; j < maxch; j += kBlk) chunk_filter[j] = kSentinel;
-  // row f: block b's first slot in filter f's run
-  const uint32_t per = (nb + kBlk - 1) / kBlk;
-  const uint32_t b0 = threadIdx.x * per, b1 = min(b0 + per, nb);
-  const uint64_t stride = F + 1;  // block-major: column f
-  uint32_t s = 0;
-  for (uint32_t b = b0; b < b1; ++b) s += cnt_[b * stride + f];
-  uint32_t total;
-  uint32_t run = (uint32_t)sq + block_excl_scan<kBlk>(s, scratch, &total);
-  for (uint32_t b = b0; b < b1; ++b) {
-    start[b * stride + f] = run;
-    run += cnt_[b * stride + f];
-  }
-}
-
 // A block's runs: filter f's queries of block b go to slots [lstart[f],
 // lstart[f] + lcnt[f]) in filter order and to places [lbase[f], ...) of the
 // block's own sorted order.  Loads lcnt, lstart (and ltiles) and scans lbase.
@@ -377,7 +305,7 @@ __global__ __launch_bounds__(kBlk) void pb_scatter_kernel(const uint4 *__restric
                                                           const uint32_t *__restrict__ cnt,
                                                           const uint32_t *__restrict__ start,
                                                           uint16_t *__restrict__ dest, uint2 *__restrict__ hs,
-                                                          uint32_t exp, uint32_t flat) {
+                                                          uint32_t exp) {
 #ifndef ADL_BLOOM_STAMPS
   exp = 0;  // diagnostics build only (wrong answers): 8 no hashing, 16 no run stores, 32 no place stores
 #endif
@@ -385,7 +313,6 @@ __global__ __launch_bounds__(kBlk) void pb_scatter_kernel(const uint4 *__restric
   uint2 *lhs = reinterpret_cast<uint2 *>(lds);  // kQB hashes in the block's filter order
   uint32_t *lcnt = lds + 2 * kQB, *lstart = lcnt + F + 1, *lbase = lstart + F + 1, *lcur = lbase + F + 1;
   uint32_t *ltiles = lcur + F + 1, *scratch = ltiles + F + 1;
-  uint16_t *lf = reinterpret_cast<uint16_t *>(scratch + 32);  // flat: filter of each place (kQB)
   const int tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid / kWave;
   // every query's id and key are requested first (unconditionally: a lane
   // past n loads the last query and discards it), so they land while the
@@ -418,25 +345,15 @@ __global__ __launch_bounds__(kBlk) void pb_scatter_kernel(const uint4 *__restric
           hash16(kq[r], h1, h2);
         }
         lhs[place] = make_uint2(h1, h2);
-        if (flat) lf[place] = (uint16_t)b;
       }
       if (!(exp & 32)) dest[i] = place;
     }
   }
   __syncthreads();
   if (exp & 16) return;
-  if (flat) {
-    // place by place: thread e writes the hashes at place e to its filter's
-    // run, so every lane of every store carries one (runs of ~32 queries
-    // filled only half a wave per store in the per-run loop below)
-    const uint32_t placed = lbase[F];
-    for (uint32_t e = tid; e < placed; e += kBlk) {
-      const uint32_t f = lf[e];
-      hs[lstart[f] + (e - lbase[f])] = lhs[e];
-    }
-    return;
-  }
-  // run by run: consecutive lanes write consecutive slots (whole lines)
+  // run by run: consecutive lanes write consecutive slots (whole lines);
+  // place by place (every lane of a store carrying one) measured the same
+  // (profiles/r04/probe_flat_k3.log)
   for (uint32_t f = wave; f < F; f += kBlk / kWave) {
     const uint32_t c = lcnt[f], lb = lbase[f], gs = lstart[f];
     for (uint32_t r = lane; r < c; r += kWave) hs[gs + r] = lhs[lb + r];
@@ -446,17 +363,16 @@ __global__ __launch_bounds__(kBlk) void pb_scatter_kernel(const uint4 *__restric
 // ---------------------------------------------------------------- P1
 // Persistent: workgroup b takes chunks b, b + G, ...; the next chunk's hashes
 // are in flight into registers while the current one is sorted and stored.
-// Rounds (the batched form of the reference's stop at the first clear bit,
-// src/filter_block.cpp:54-59): round 0 bins all k bits of every query; round 1
-// bins bits j0 .. j0+KFIX of every query and sets its answer to 1; round 2
-// bins bits j0 .. j0+KFIX of the queries whose answer round 1's pb_tile left
-// at 1.  KFIX = 0: all k bits, round 0 only.
+// All k bits of every query are binned in one round (the reference stops at
+// the first clear bit, src/filter_block.cpp:54-59; the answer is the AND
+// either way, and a two-round form measured slower: DESIGN.md §5).  KFIX = 0:
+// runtime k.
 template <int KFIX>
 __global__ __launch_bounds__(kBlk) void pb_bin_kernel(const uint2 *__restrict__ hs, const PFilter *__restrict__ desc,
                                                       const uint32_t *__restrict__ chunk_filter,
                                                       const uint32_t *__restrict__ scal, uint32_t k, uint32_t C,
                                                       uint32_t *__restrict__ ent, uint32_t *__restrict__ table,
-                                                      uint8_t *__restrict__ res, uint32_t j0, uint32_t round) {
+                                                      uint8_t *__restrict__ res) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   uint32_t *hist = lds;                          // kMaxTiles + 1 counters, later cursors
   uint32_t *scratch = lds + kMaxTiles + 4;       // scan scratch (64 words)
@@ -466,32 +382,25 @@ __global__ __launch_bounds__(kBlk) void pb_bin_kernel(const uint2 *__restrict__ 
   const int tid = threadIdx.x;
   const uint32_t total_chunks = scal[1];
   const uint32_t G = gridDim.x;
-  // the answers round 1 left (round 2), loaded with the hashes; answers are one
-  // "cleared" bit per slot (1: a tested bit was clear, the answer is 0)
-  const bool filt = round == 2;
+  // answers are one "cleared" bit per slot (1: a tested bit was clear, the answer is 0)
   uint32_t *clrw = reinterpret_cast<uint32_t *>(res);
-  auto fetch = [&](uint32_t c, uint2 (&h)[kCPT], uint8_t (&al)[kCPT]) {
+  auto fetch = [&](uint32_t c, uint2 (&h)[kCPT]) {
     if (c >= total_chunks) return;
     const uint32_t f = chunk_filter[c];
     const uint32_t j = c - desc[f].chunk_base;
     const uint32_t q0 = desc[f].qbase + j * C;
     const uint32_t cnt = min(C, desc[f].cnt - j * C);
 #pragma unroll
-    for (uint32_t r = 0; r < kCPT; ++r) {
-      const uint32_t q = q0 + min(tid + r * kBlk, cnt - 1u);
-      h[r] = hs[q];
-      al[r] = filt ? (uint8_t)(((clrw[q >> 5] >> (q & 31)) & 1u) ^ 1u) : (uint8_t)1;
-    }
+    for (uint32_t r = 0; r < kCPT; ++r) h[r] = hs[q0 + min(tid + r * kBlk, cnt - 1u)];
   };
   uint2 nxt[kCPT];
-  uint8_t nal[kCPT];
-  fetch(blockIdx.x, nxt, nal);
+  fetch(blockIdx.x, nxt);
   for (uint32_t c = blockIdx.x; c < total_chunks; c += G) {
     uint2 cur[kCPT];
     bool live[kCPT];
 #pragma unroll
-    for (uint32_t r = 0; r < kCPT; ++r) cur[r] = nxt[r], live[r] = nal[r] != 0;
-    fetch(c + G, nxt, nal);
+    for (uint32_t r = 0; r < kCPT; ++r) cur[r] = nxt[r], live[r] = true;
+    fetch(c + G, nxt);
     const uint32_t f = chunk_filter[c];
     const PFilter d = desc[f];
     const uint32_t j = c - d.chunk_base;
@@ -503,7 +412,7 @@ __global__ __launch_bounds__(kBlk) void pb_bin_kernel(const uint2 *__restrict__ 
     for (uint32_t t = tid; t <= T; t += kBlk) hist[t] = 0;
     // the chunk's cleared bits start at 0 (the words it shares with its
     // neighbours are zeroed by both, before any pb_tile)
-    if (!filt && cnt)
+    if (cnt)
       for (uint32_t wd = (q0 >> 5) + tid; wd <= ((q0 + cnt - 1u) >> 5); wd += kBlk) clrw[wd] = 0u;
 #pragma unroll
     for (uint32_t r = 0; r < kCPT; ++r) live[r] = live[r] && tid + r * kBlk < cnt;
@@ -515,7 +424,7 @@ __global__ __launch_bounds__(kBlk) void pb_bin_kernel(const uint2 *__restrict__ 
         if constexpr (KFIX > 0) {
 #pragma unroll
           for (int jj = 0; jj < KFIX; ++jj) {
-            pos[r][jj] = fastmod(cur[r].x + (j0 + (uint32_t)jj) * cur[r].y, mod);
+            pos[r][jj] = fastmod(cur[r].x + (uint32_t)jj * cur[r].y, mod);
             atomicAdd(&hist[pos[r][jj] >> kTL], 1u);
           }
         } else {
@@ -880,79 +789,43 @@ int adl_bloom_probe_batch_device(const uint8_t *d_keys, const uint64_t *d_offset
   const uint32_t cus = adl_host::device_cus();
   const size_t lds_k1 = (size_t)(2 * F + 2) * 4;                       // counters + tile counts
   const size_t lds_k3 = (size_t)(2 * kQB + 5 * (F + 1) + 32) * 4;      // hashes + 5 per-filter arrays + scratch
-  // + a 2-byte filter id per place: K3 then writes its runs place by place
-  // (ADL_PB_FLAT=1; default: run by run)
-  const bool k3_flat = lds_k3 + kQB * 2 <= (size_t)kLdsWords * 4 && adl_host::env_on("ADL_PB_FLAT", false);
   const size_t lds_k6 = (size_t)(kQB / 4 + 3 * (F + 1) + 32) * 4;      // answers + 3 per-filter arrays + scratch
   const size_t lds_p1 = (size_t)(kMaxTiles + 4 + 64 + p.k * p.C) * 4;
   const size_t lds_p2 = (size_t)kTileBytes + 64 + (size_t)((F + 1 + 3) & ~3u) * 4 +
                         (size_t)(kBlk / kWave) * kMaskWords * 4;
+#ifdef ADL_BLOOM_STAMPS
+  const uint32_t exp = adl_host::knobs().pb_exp;  // diagnostics build only
+#else
+  constexpr uint32_t exp = 0;
+#endif
   try {
     hipLaunchKernelGGL(pb_desc_kernel, dim3(1), dim3(kBlk), 0, st, d_bitmap_off, d_bitmap_end, F, desc, scal);
     ADL_HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(pb_hist_kernel, dim3(p.nb), dim3(kBlk), lds_k1, st, d_filter_id, n, F, p.nb, desc, cnt);
     ADL_HIP_TRY(hipGetLastError());
-#ifdef ADL_BLOOM_STAMPS
-    const bool old_scan = getenv("ADL_PB_OLDSCAN") != nullptr;  // diagnostics build: round-2 K2 (A/B)
-#else
-    constexpr bool old_scan = false;
-#endif
-    if (old_scan) {
-      hipLaunchKernelGGL(pb_rows_kernel, dim3(F + 1), dim3(256), 0, st, cnt, p.nb, F, desc);
-      ADL_HIP_TRY(hipGetLastError());
-      hipLaunchKernelGGL(pb_scan_kernel, dim3(F + 1), dim3(kBlk), 0, st, cnt, start, p.nb, F, p.C, p.maxch, desc, cf,
-                         scal);
-      ADL_HIP_TRY(hipGetLastError());
-    } else {
-      uint32_t *gsum = reinterpret_cast<uint32_t *>(ws + p.o_gsum);
-      hipLaunchKernelGGL(pb_colsum_kernel, dim3(p.ng), dim3(kBlk), 0, st, cnt, p.nb, F, gsum);
-      ADL_HIP_TRY(hipGetLastError());
-      hipLaunchKernelGGL(pb_plan_kernel, dim3(1), dim3(kBlk), 0, st, gsum, p.ng, F, p.C, p.maxch, desc, cf, scal);
-      ADL_HIP_TRY(hipGetLastError());
-      hipLaunchKernelGGL(pb_starts_kernel, dim3(p.ng), dim3(kBlk), 0, st, cnt, gsum, p.nb, F, desc, start);
-      ADL_HIP_TRY(hipGetLastError());
-    }
-    if (int rc = adl_host::lds_limit<pb_scatter_kernel>()) return rc;
-#ifdef ADL_BLOOM_STAMPS
-    const char *exp_env = getenv("ADL_PB_EXP");  // diagnostics build only
-    const uint32_t exp = exp_env ? (uint32_t)atoi(exp_env) : 0u;
-#else
-    constexpr uint32_t exp = 0;
-#endif
-    hipLaunchKernelGGL(pb_scatter_kernel, dim3(p.nb), dim3(kBlk), lds_k3 + (k3_flat ? kQB * 2 : 0), st, reinterpret_cast<const uint4 *>(d_keys),
-                       d_filter_id, n, F, p.nb, desc, cnt, start, dest, hs, exp, k3_flat ? 1u : 0u);
+    uint32_t *gsum = reinterpret_cast<uint32_t *>(ws + p.o_gsum);
+    hipLaunchKernelGGL(pb_colsum_kernel, dim3(p.ng), dim3(kBlk), 0, st, cnt, p.nb, F, gsum);
     ADL_HIP_TRY(hipGetLastError());
-    // k = 6: two rounds, bits 0 .. split-1 of every query, then the rest for
-    // the queries still answered 1 (ADL_PB_SPLIT = 0: one round of all k)
-    // (a tuning knob read per call so tests can flip it; a value other than
-    // 0, 1, 2 is ignored)
-    const char *split_env = getenv("ADL_PB_SPLIT");
-    uint32_t split = split_env ? (uint32_t)atoi(split_env) : kSplit6;
-    if (p.k != 6 || split > 2) split = p.k == 6 ? kSplit6 : 0u;
+    hipLaunchKernelGGL(pb_plan_kernel, dim3(1), dim3(kBlk), 0, st, gsum, p.ng, F, p.C, p.maxch, desc, cf, scal);
+    ADL_HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(pb_starts_kernel, dim3(p.ng), dim3(kBlk), 0, st, cnt, gsum, p.nb, F, desc, start);
+    ADL_HIP_TRY(hipGetLastError());
+    if (int rc = adl_host::lds_limit<pb_scatter_kernel>()) return rc;
+    hipLaunchKernelGGL(pb_scatter_kernel, dim3(p.nb), dim3(kBlk), lds_k3, st, reinterpret_cast<const uint4 *>(d_keys),
+                       d_filter_id, n, F, p.nb, desc, cnt, start, dest, hs, exp);
+    ADL_HIP_TRY(hipGetLastError());
     if (int rc = adl_host::lds_limit<pb_tile_kernel>()) return rc;
-    using BinK = decltype(&pb_bin_kernel<6>);
-    auto bin = [&](BinK kern, int lds_rc, uint32_t j0, uint32_t round) -> int {
-      if (lds_rc) return lds_rc;
-      hipLaunchKernelGGL(kern, dim3(cus), dim3(kBlk), lds_p1, st, hs, desc, cf, scal, p.k, p.C, ent, tab, res, j0,
-                         round);
+    auto bin = [&](auto lim, auto kern) -> int {
+      if (int rc = lim()) return rc;
+      hipLaunchKernelGGL(kern, dim3(cus), dim3(kBlk), lds_p1, st, hs, desc, cf, scal, p.k, p.C, ent, tab, res);
       ADL_HIP_TRY(hipGetLastError());
       hipLaunchKernelGGL(pb_tile_kernel, dim3(cus), dim3(kBlk), lds_p2, st, d_bitmaps, desc, F, scal, p.k, p.C, ent,
                          tab, res, exp);
       ADL_HIP_TRY(hipGetLastError());
       return ADL_OK;
     };
-    int rc_bin;
-    if (split == 1) {
-      if ((rc_bin = bin(pb_bin_kernel<1>, adl_host::lds_limit<pb_bin_kernel<1>>(), 0u, 1u)) != ADL_OK) return rc_bin;
-      rc_bin = bin(pb_bin_kernel<5>, adl_host::lds_limit<pb_bin_kernel<5>>(), 1u, 2u);
-    } else if (split == 2) {
-      if ((rc_bin = bin(pb_bin_kernel<2>, adl_host::lds_limit<pb_bin_kernel<2>>(), 0u, 1u)) != ADL_OK) return rc_bin;
-      rc_bin = bin(pb_bin_kernel<4>, adl_host::lds_limit<pb_bin_kernel<4>>(), 2u, 2u);
-    } else if (p.k == 6) {
-      rc_bin = bin(pb_bin_kernel<6>, adl_host::lds_limit<pb_bin_kernel<6>>(), 0u, 0u);
-    } else {
-      rc_bin = bin(pb_bin_kernel<0>, adl_host::lds_limit<pb_bin_kernel<0>>(), 0u, 0u);
-    }
+    const int rc_bin = p.k == 6 ? bin(adl_host::lds_limit<pb_bin_kernel<6>>, pb_bin_kernel<6>)
+                                : bin(adl_host::lds_limit<pb_bin_kernel<0>>, pb_bin_kernel<0>);
     if (rc_bin != ADL_OK) return rc_bin;
     if (int rc = adl_host::lds_limit<pb_gather_kernel>()) return rc;
     hipLaunchKernelGGL(pb_gather_kernel, dim3(p.nb), dim3(kBlk), lds_k6, st, dest, res, n, F, p.nb, cnt, start,

@@ -19,20 +19,28 @@
 //                    above the 8 answer bits.  Both in one 8-byte system-scope
 //                    store; the host takes its answers from word 1 alone
 //
-// The wave polls the bells, copies every pending slot into LDS with one load
-// per lane per slot (one round trip for all of them), hashes each query's key
-// from LDS (hash_bytes), tests its k bits in the arena with all k loads in
-// flight at once, writes the answers and then the sequence numbers.  The host
+// The wave polls the bells, copies pending slots into LDS four at a time (one
+// load per lane per slot, one round trip for the group), hashes each query's
+// key from LDS (hash_bytes), tests its k bits in the arena with eight loads in
+// flight at once, and writes the answers with the sequence numbers.  The host
 // thread spins on its done line.
 //
-// Lifetime.  The kernel exits when it has been idle for idle_ticks, when it has
-// run for life_ticks, or when the host raises ctl->stop (cache teardown), so
-// its wave always finishes.  A host thread whose request is not answered
-// checks the server's completion event: if the kernel has exited (idle or
-// life limit) it launches a new one, which picks up the pending request; if
-// the event reports an error, the call fails with ADL_ERR_DEVICE.  The server
-// runs on a stream of its own, created with a CU mask, so no other stream's
-// work queues behind it on a shared hardware queue.
+// Lifetime.  The kernel leaves when it has been idle for idle_ticks, when it
+// has run for life_ticks, or when the host raises ctl->stop (cache teardown),
+// so its wave always finishes.  Leaving, it clears ctl->alive and then polls
+// once more, serving what it finds.  A host thread rings its bell and then
+// reads alive: 1 means the kernel's next poll sees the bell; 0 means it waits
+// for the kernel to end (that last poll may have answered it) and launches a
+// new one if not.  So an exit costs a request one relaunch, never a timeout;
+// the unanswered-for-50-us check is left for a kernel that failed (its
+// completion event reports the error: ADL_ERR_DEVICE).
+//
+// Footprint.  2 KiB of LDS and 32 VGPRs: the wave fits on a CU beside a
+// build's persistent pass-A workgroup, which leaves exactly that free, so a
+// Get is served while a compaction builds (reference: DB::Get probes filters
+// without a lock while DoCompaction runs, src/db.cpp:164-172, 263, 294).  The
+// server runs on a stream of its own, created with a CU mask (all CUs), so no
+// other stream's work queues behind it on a shared hardware queue.
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -53,6 +61,7 @@ namespace {
 
 constexpr uint32_t kSlots = 64;      // one per lane of the server wave
 constexpr uint32_t kSlotBytes = 512;
+constexpr uint32_t kGroup = 4;       // slots staged in LDS at a time (2 KiB)
 constexpr uint32_t kHdrBytes = 16;   // seq (unused by the device), n, k, key bytes
 constexpr uint32_t kRangeOff = kHdrBytes;                      // u64 begin, end per query
 constexpr uint32_t kKoffOff = kRangeOff + 16 * adl_srv::kMaxQ;  // u16 offsets, kMaxQ + 1
@@ -77,8 +86,9 @@ static_assert(adl_srv::kMaxQ == 8, "a done word holds 8 answer bits");
 
 struct Ctl {
   uint32_t stop[16];  // replicated: lane l reads stop[l % 16] (a per-lane, vector load)
-  uint32_t alive;     // host: 1 before a launch; kernel: 0 as it returns
-  uint32_t pad[15];
+  uint32_t alive;     // host: 1 before a launch; kernel: 0 as it leaves (before its last poll)
+  uint32_t gen_done;  // kernel: its launch generation, after its last poll's answers
+  uint32_t pad[14];
 };
 
 // The shared area, one hipHostMalloc (mapped, coherent): bells, control, done
@@ -96,97 +106,118 @@ __device__ __forceinline__ uint32_t ld_sys(const uint32_t *p) {
 
 __device__ __forceinline__ uint64_t now_ticks() { return __builtin_amdgcn_s_memrealtime(); }  // 100 MHz
 
-// One wave.  Lane l polls bell l; LDS holds a copy of every pending slot.
-__global__ __launch_bounds__(64) void probe_server_kernel(Area *area, uint64_t idle_ticks, uint64_t life_ticks) {
-  __shared__ __attribute__((aligned(16))) uint8_t lslot[kSlots][kSlotBytes];
-  __shared__ uint8_t lans[kSlots][adl_srv::kMaxQ];
+// Query q of a slot staged in LDS: 1 iff all k bits of its filter range are set.
+__device__ __forceinline__ uint32_t serve_query(const Slot &sl, uint32_t q) {
+  const uint32_t k = min(sl.k, 30u);
+  const uint64_t b0 = sl.range[2 * q], b1 = sl.range[2 * q + 1];
+  // 0 for an empty range or a filter of 2^31 bits or more (src/filter_block.cpp:50)
+  const uint32_t mbits = b1 > b0 && b1 - b0 <= 0x0fffffffull ? (uint32_t)((b1 - b0) * 8) : 0u;
+  if (!mbits) return 0;
+  const uint32_t ko = min((uint32_t)sl.koff[q], adl_srv::kMaxKeyBytes);
+  const uint32_t ke = min(max((uint32_t)sl.koff[q + 1], ko), adl_srv::kMaxKeyBytes);
+  uint32_t h1, h2;
+  hash_bytes(sl.keys + ko, ke - ko, kSeed1, kSeed2, h1, h2);
+  const FastMod mod = fastmod_for(mbits);
+  const uint8_t *bm = reinterpret_cast<const uint8_t *>(b0);
+  // the answer is the AND of the k bits (src/filter_block.cpp:54-59; the
+  // early exit changes no answer): 8 reads in flight at a time
+  uint32_t all = 1;
+  for (uint32_t g = 0; g < k; g += 8) {
+    uint32_t w[8];
+#pragma unroll
+    for (uint32_t u = 0; u < 8; ++u) {
+      const uint32_t p = fastmod(h1 + (g + u < k ? g + u : 0u) * h2, mod);  // past k: bit 0 again
+      w[u] = (uint32_t)(bm[p >> 3] >> (p & 7));
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < 8; ++u) all &= w[u];
+  }
+  return all & 1u;
+}
+
+// One wave.  Lane l polls bell l.  Pending slots are staged kGroup at a time
+// in 2 KiB of LDS (one 8-byte load per lane per slot, all in flight at once);
+// lane 8u + q then answers query q of the group's slot u.  The small footprint
+// (2 KiB of LDS, 32 VGPRs) lets the wave run beside a build's persistent
+// workgroups, which leave exactly that much of their CU free (bloom_build.hip,
+// kLdsReserveWords): a Get does not wait for a build.
+__global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(16))) void probe_server_kernel(
+    Area *area, uint64_t idle_ticks, uint64_t life_ticks, uint32_t gen) {
+  __shared__ __attribute__((aligned(16))) uint8_t lslot[kGroup][kSlotBytes];
   const uint32_t lane = threadIdx.x;
   uint32_t served = __hip_atomic_load(&area->done[lane].seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   const uint64_t t0 = now_ticks();
   uint64_t last = t0;
+  bool closing = false;
   for (;;) {
     const uint32_t bell = ld_sys(&area->bell[lane]);
     const bool pend = bell != served;
     const uint64_t pm = __ballot(pend);
     if (pm == 0) {
+      if (closing) break;
       const uint64_t t = now_ticks();
       const bool stop = __ballot(ld_sys(&area->ctl.stop[lane & 15]) != 0) != 0;
-      if (stop || t - last > idle_ticks || t - t0 > life_ticks) break;
+      if (stop || t - last > idle_ticks || t - t0 > life_ticks) {
+        // Leaving: alive = 0 first, then one more poll, whose bells are
+        // served before the wave ends.  A host thread rings its bell and then
+        // reads alive (both sequentially consistent): if it read 1, this
+        // poll sees its bell; if it read 0, it waits for this kernel to end
+        // and relaunches only if its request is still unanswered.
+        if (lane == 0) __hip_atomic_store(&area->ctl.alive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "");
+        closing = true;
+        continue;
+      }
       __builtin_amdgcn_s_sleep(1);
       continue;
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // the slots were written before their bells
-    // copy every pending slot into LDS: 8 bytes per lane per slot, 8 slots' loads in flight at a time
     for (uint64_t m = pm; m;) {
-      uint32_t js[8];
-      uint64_t v[8];
+      uint32_t js[kGroup];
+      uint64_t v[kGroup];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
+      for (uint32_t u = 0; u < kGroup; ++u) {
         js[u] = m ? (uint32_t)__builtin_ctzll(m) : kSlots;
         m &= m - 1;  // (m = 0 stays 0)
         const uint64_t *src = reinterpret_cast<const uint64_t *>(&area->slot[js[u] < kSlots ? js[u] : 0]);
         v[u] = __hip_atomic_load(src + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       }
 #pragma unroll
-      for (int u = 0; u < 8; ++u)
-        if (js[u] < kSlots) reinterpret_cast<uint64_t *>(lslot[js[u]])[lane] = v[u];
-    }
-    __syncthreads();
-    // one lane per (slot, query): slot j's query q is lane (q * 64 + j) % ...;
-    // simply: every lane walks the pending slots and takes query `lane % kMaxQ`
-    // of slot (8 * r + lane / kMaxQ) in round r
-    const uint32_t npend = __popcll(pm);
-    for (uint32_t r = 0; r * (64 / adl_srv::kMaxQ) < npend; ++r) {
-      const uint32_t which = r * (64 / adl_srv::kMaxQ) + lane / adl_srv::kMaxQ;  // index among pending slots
-      const uint32_t q = lane % adl_srv::kMaxQ;
-      if (which >= npend) continue;
-      uint64_t m = pm;
-      for (uint32_t s = 0; s < which; ++s) m &= m - 1;
-      const uint32_t j = __builtin_ctzll(m);
-      const Slot &sl = *reinterpret_cast<const Slot *>(lslot[j]);
-      const uint32_t n = min(sl.n, adl_srv::kMaxQ);
-      if (q >= n) continue;
-      const uint32_t k = min(sl.k, 30u);
-      const uint64_t b0 = sl.range[2 * q], b1 = sl.range[2 * q + 1];
-      // 0 for an empty range or a filter of 2^31 bits or more (src/filter_block.cpp:50)
-      const uint32_t mbits = b1 > b0 && b1 - b0 <= 0x0fffffffull ? (uint32_t)((b1 - b0) * 8) : 0u;
-      uint8_t hit = 0;
-      const uint32_t ko = min((uint32_t)sl.koff[q], adl_srv::kMaxKeyBytes);
-      const uint32_t ke = min(max((uint32_t)sl.koff[q + 1], ko), adl_srv::kMaxKeyBytes);
-      if (mbits) {
-        uint32_t h1, h2;
-        hash_bytes(sl.keys + ko, ke - ko, kSeed1, kSeed2, h1, h2);
-        const FastMod mod = fastmod_for(mbits);
-        const uint8_t *bm = reinterpret_cast<const uint8_t *>(b0);
-        // all reads in flight together (the answer is the AND of the k bits,
-        // src/filter_block.cpp:54-59; the early exit changes no answer); bits
-        // past k repeat bit 0
-        uint32_t all = 1;
+      for (uint32_t u = 0; u < kGroup; ++u) reinterpret_cast<uint64_t *>(lslot[u])[lane] = v[u];
+      __syncthreads();
+      const uint32_t u = lane / adl_srv::kMaxQ, q = lane % adl_srv::kMaxQ;
+      uint32_t j = kSlots;  // the slot lane 8u + q serves (kSlots: none)
 #pragma unroll
-        for (uint32_t g = 0; g < 30; ++g) {
-          const uint32_t p = fastmod(h1 + (g < k ? g : 0u) * h2, mod);
-          all &= (uint32_t)(bm[p >> 3] >> (p & 7));
-        }
-        hit = (uint8_t)(all & 1u);
+      for (uint32_t x = 0; x < kGroup; ++x) j = u == x ? js[x] : j;
+      uint32_t hit = 0;
+      if (j < kSlots) {
+        const Slot &sl = *reinterpret_cast<const Slot *>(lslot[u]);
+        if (q < min(sl.n, adl_srv::kMaxQ)) hit = serve_query(sl, q);
       }
-      lans[j][q] = hit;
-    }
-    __syncthreads();
-    // the answers: one 8-byte system-scope store (a plain store can sit in the
-    // device's write path while the wave keeps polling: the host then sees it
-    // only when the kernel ends)
-    if (pend) {
-      uint32_t bits = 0;
+      const uint64_t hb = __ballot(hit != 0);
+      // lane u < kGroup answers slot js[u]: {seq, (seq << 8) | answer bits} in
+      // one 8-byte system-scope store (a plain store can sit in the device's
+      // write path while the wave keeps polling)
+      uint32_t ju = kSlots;
 #pragma unroll
-      for (uint32_t q = 0; q < adl_srv::kMaxQ; ++q) bits |= (uint32_t)(lans[lane][q] & 1u) << q;
-      const uint64_t v = (uint64_t)bell | ((uint64_t)((bell << 8) | bits) << 32);
-      __hip_atomic_store(reinterpret_cast<uint64_t *>(&area->done[lane]), v, __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_SYSTEM);
-      served = bell;
+      for (uint32_t x = 0; x < kGroup; ++x) ju = lane == x ? js[x] : ju;
+      const uint32_t seq = (uint32_t)__shfl((int)bell, (int)(ju < kSlots ? ju : 0u));
+      if (ju < kSlots) {
+        const uint32_t bits = (uint32_t)(hb >> (lane * adl_srv::kMaxQ)) & 0xFFu;
+        const uint64_t word = (uint64_t)seq | ((uint64_t)((seq << 8) | bits) << 32);
+        __hip_atomic_store(reinterpret_cast<uint64_t *>(&area->done[ju]), word, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+      __syncthreads();  // the group's LDS copy is read before the next group overwrites it
     }
+    if (pend) served = bell;
     last = now_ticks();
+    if (closing) break;
   }
-  if (lane == 0) __hip_atomic_store(&area->ctl.alive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  // the last poll's answers are out: the host may launch the next kernel (on
+  // the other stream) as soon as it sees this
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  if (lane == 0) __hip_atomic_store(&area->ctl.gen_done, gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 }  // namespace
@@ -197,8 +228,14 @@ struct Server {
   Area *host = nullptr;  // mapped, coherent
   Area *dev = nullptr;   // its device address
   hipStream_t stream = nullptr;
-  hipEvent_t exited = nullptr;  // completes when the running kernel returns
+  // Completion events of the kernels, by generation parity: a relaunch is
+  // queued while its predecessor's dispatch may still be completing, and an
+  // event still pending must not be recorded again (that left
+  // hipStreamDestroy waiting at teardown now and then).  The kernel two
+  // generations back has completed before its successor started.
+  hipEvent_t exited[2] = {};
   bool launched = false;
+  uint32_t gen = 0;  // the latest kernel's launch generation (Ctl::gen_done)
   int device = 0;
   std::mutex launch_mu;
   std::mutex slot_mu[kSlots];
@@ -210,6 +247,8 @@ struct Server {
 
 namespace {
 
+std::atomic<uint64_t> g_launches{0};
+
 void set_stop(Server *s, uint32_t v) {
   for (uint32_t &w : s->host->ctl.stop) __atomic_store_n(&w, v, __ATOMIC_SEQ_CST);
 }
@@ -217,36 +256,77 @@ void set_stop(Server *s, uint32_t v) {
 std::mutex g_reg_mu;
 std::vector<Server *> *g_reg = nullptr;
 
+void wait_all(Server *s) {
+  if (!s->launched) return;
+  (void)hipEventSynchronize(s->exited[(s->gen + 1) & 1]);
+  (void)hipEventSynchronize(s->exited[s->gen & 1]);
+}
+
 void stop_all_at_exit() {
   std::lock_guard<std::mutex> g(g_reg_mu);
   if (!g_reg) return;
   for (Server *s : *g_reg) {
     set_stop(s, 1);
-    if (s->launched) (void)hipEventSynchronize(s->exited);
+    wait_all(s);
   }
 }
 
-uint64_t env_us(const char *name, uint64_t dflt) {
-  const char *e = getenv(name);
-  return e ? strtoull(e, nullptr, 10) : dflt;
+bool answered(const Server *s, uint32_t my, uint32_t seq, uint32_t *bits) {
+  const uint32_t w = __atomic_load_n(&s->host->done[my].tagged, __ATOMIC_ACQUIRE);
+  if ((w >> 8) != (seq & 0xFFFFFFu)) return false;
+  *bits = w & 0xFFu;
+  return true;
 }
 
-// Launch a server kernel unless one is running (caller holds launch_mu).
-int ensure_running(Server *s) {
+// The caller saw alive == 0 after ringing bell `my` (or waited long): make
+// sure a kernel will answer it.  Caller holds launch_mu.  A kernel that
+// cleared alive is in its last poll or gone: wait until it has published its
+// generation (its last answers are out by then; no wait for its completion
+// event), then launch the next one unless that last poll answered the
+// request.  *done = answered.
+int ensure_running(Server *s, uint32_t my, uint32_t seq, uint32_t *bits, bool *done) {
+  *done = false;
   if (s->launched) {
-    const hipError_t q = hipEventQuery(s->exited);
-    if (q == hipErrorNotReady) return ADL_OK;
-    if (q != hipSuccess) {
-      (void)hipGetLastError();
-      return ADL_ERR_DEVICE;
+    hipEvent_t ev = s->exited[s->gen & 1];
+    if (__atomic_load_n(&s->host->ctl.alive, __ATOMIC_SEQ_CST)) {
+      // alive: a kernel launched since (or not yet started) will poll the bell,
+      // unless it has failed
+      const hipError_t q = hipEventQuery(ev);
+      if (q == hipErrorNotReady) return ADL_OK;
+      if (q != hipSuccess) {
+        (void)hipGetLastError();
+        return ADL_ERR_DEVICE;
+      }
+    } else {
+      // leaving: its generation word comes a poll later (a kernel that failed
+      // in between never writes it: its event reports the error)
+      const auto t0 = std::chrono::steady_clock::now();
+      for (uint32_t spin = 0; __atomic_load_n(&s->host->ctl.gen_done, __ATOMIC_ACQUIRE) != s->gen; ++spin) {
+        __builtin_ia32_pause();
+        if (spin % 1024 == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(500)) {
+          const hipError_t q = hipEventQuery(ev);
+          if (q == hipSuccess) break;
+          if (q != hipErrorNotReady) {
+            (void)hipGetLastError();
+            return ADL_ERR_DEVICE;
+          }
+        }
+      }
+    }
+    if (answered(s, my, seq, bits)) {
+      *done = true;
+      return ADL_OK;
     }
   }
   set_stop(s, 0);
   __atomic_store_n(&s->host->ctl.alive, 1u, __ATOMIC_SEQ_CST);
-  hipExtLaunchKernelGGL(probe_server_kernel, dim3(1), dim3(64), 0, s->stream, nullptr, s->exited, 0, s->dev,
-                        s->idle_ticks, s->life_ticks);
-  if (hipGetLastError() != hipSuccess) return ADL_ERR_DEVICE;
+  const uint32_t gen = s->gen + 1;
+  hipLaunchKernelGGL(probe_server_kernel, dim3(1), dim3(64), 0, s->stream, s->dev, s->idle_ticks, s->life_ticks, gen);
+  if (hipGetLastError() != hipSuccess || hipEventRecord(s->exited[gen & 1], s->stream) != hipSuccess)
+    return ADL_ERR_DEVICE;
   s->launched = true;
+  s->gen = gen;
+  g_launches.fetch_add(1, std::memory_order_relaxed);
   return ADL_OK;
 }
 
@@ -256,7 +336,8 @@ Server *create() {
   auto *s = new (std::nothrow) Server;
   if (!s) return nullptr;
   auto fail = [&]() -> Server * {
-    if (s->exited) (void)hipEventDestroy(s->exited);
+    for (hipEvent_t e : s->exited)
+      if (e) (void)hipEventDestroy(e);
     if (s->stream) (void)hipStreamDestroy(s->stream);
     if (s->host) (void)hipHostFree(s->host);
     (void)hipGetLastError();
@@ -272,16 +353,22 @@ Server *create() {
     return fail();
   memset(s->host, 0, sizeof(Area));
   s->dev = static_cast<Area *>(d);
-  // a CU-masked stream gets a hardware queue of its own (all CUs enabled)
-  std::vector<uint32_t> mask((adl_host::device_cus() + 31) / 32, ~0u);
-  if (hipExtStreamCreateWithCUMask(&s->stream, (uint32_t)mask.size(), mask.data()) != hipSuccess) {
+  // A stream of the highest priority: its hardware queue is not shared with
+  // the process's ordinary streams, so no other stream's work waits behind
+  // the resident kernel.  (A CU-masked stream does that too, but after a few
+  // relaunches on one the process hung at exit, in the runtime's teardown,
+  // every time: profiles/r05/server_stream_exit.log.)
+  int lo = 0, hi = 0;
+  if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess ||
+      hipStreamCreateWithPriority(&s->stream, hipStreamNonBlocking, hi) != hipSuccess) {
     (void)hipGetLastError();
     if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess) return fail();
   }
-  if (hipEventCreateWithFlags(&s->exited, hipEventDisableTiming) != hipSuccess) return fail();
+  for (hipEvent_t &e : s->exited)
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return fail();
   // 100 MHz ticks: idle 2 ms, life 20 ms by default
-  s->idle_ticks = env_us("ADL_BLOOM_SERVER_IDLE_US", 2000) * 100;
-  s->life_ticks = env_us("ADL_BLOOM_SERVER_LIFE_US", 20000) * 100;
+  s->idle_ticks = adl_host::knobs().server_idle_us * 100;
+  s->life_ticks = adl_host::knobs().server_life_us * 100;
   std::lock_guard<std::mutex> g(g_reg_mu);
   if (!g_reg) {
     g_reg = new std::vector<Server *>;
@@ -302,8 +389,9 @@ void destroy(Server *s) {
       }
   }
   set_stop(s, 1);
-  if (s->launched) (void)hipEventSynchronize(s->exited);
-  (void)hipEventDestroy(s->exited);
+  wait_all(s);
+  (void)hipStreamSynchronize(s->stream);
+  for (hipEvent_t e : s->exited) (void)hipEventDestroy(e);
   (void)hipStreamDestroy(s->stream);
   (void)hipHostFree(s->host);
   (void)hipGetLastError();
@@ -311,6 +399,13 @@ void destroy(Server *s) {
 }
 
 bool eligible(uint64_t n, uint64_t key_bytes) { return n >= 1 && n <= kMaxQ && key_bytes <= kMaxKeyBytes; }
+
+uint64_t launches() { return g_launches.load(std::memory_order_relaxed); }
+
+uint32_t live_servers() {
+  std::lock_guard<std::mutex> g(g_reg_mu);
+  return g_reg ? (uint32_t)g_reg->size() : 0u;
+}
 
 int probe(Server *s, const uint8_t *h_keys, const uint64_t *h_offsets, uint32_t key_stride, uint64_t n,
           const uint64_t *range, uint32_t k, uint8_t *h_out) {
@@ -337,36 +432,38 @@ int probe(Server *s, const uint8_t *h_keys, const uint64_t *h_offsets, uint32_t 
   sl.koff[n] = (uint16_t)key_bytes;
   memcpy(sl.keys, h_keys + (h_offsets ? h_offsets[0] : 0), key_bytes);
   const uint32_t seq = ++s->seq[my] == 0 ? ++s->seq[my] : s->seq[my];  // never 0 (the initial done)
+  // bell, then alive, both sequentially consistent (the kernel clears alive
+  // and then polls once more: probe_server_kernel)
   __atomic_store_n(&s->host->bell[my], seq, __ATOMIC_SEQ_CST);
-  // a running kernel keeps alive at 1 (cheaper than querying its event every
-  // call); one that is just exiting is caught by the 50 us check below
-  if (!__atomic_load_n(&s->host->ctl.alive, __ATOMIC_ACQUIRE)) {
+  uint32_t bits = 0;
+  bool done = false;
+  if (!__atomic_load_n(&s->host->ctl.alive, __ATOMIC_SEQ_CST)) {
     std::lock_guard<std::mutex> g(s->launch_mu);
-    if (int rc = ensure_running(s)) return rc;
+    if (int rc = ensure_running(s, my, seq, &bits, &done)) return rc;
   }
-  volatile Done *dn = &s->host->done[my];
   const auto t0 = std::chrono::steady_clock::now();
   auto since = [&] { return std::chrono::steady_clock::now() - t0; };
   uint32_t spins = 0;
-  uint32_t bits = 0;
-  for (;;) {
-    const uint32_t w = __atomic_load_n(&dn->tagged, __ATOMIC_ACQUIRE);
-    if ((w >> 8) == (seq & 0xFFFFFFu)) {
-      bits = w & 0xFFu;
-      break;
-    }
+  while (!done) {
+    if (answered(s, my, seq, &bits)) break;
     __builtin_ia32_pause();
     if (++spins % 4096) continue;
-    // not answered yet: a server that exited (idle / life limit) before it saw
-    // this bell is relaunched; a failed one fails the call
+    // unanswered for long (a kernel that failed, or one starved of its CU):
+    // check the kernel; past kTimeout the caller probes by a launch instead
     if (since() > std::chrono::microseconds(50)) {
       std::lock_guard<std::mutex> g(s->launch_mu);
-      if (int rc = ensure_running(s)) return rc;
+      if (int rc = ensure_running(s, my, seq, &bits, &done)) return rc;
     }
-    if (since() > std::chrono::seconds(2)) return ADL_ERR_DEVICE;
+    if (since() > kTimeout) return kBusy;
   }
   for (uint64_t q = 0; q < n; ++q) h_out[q] = (uint8_t)((bits >> q) & 1u);
   return ADL_OK;
 }
 
 }  // namespace adl_srv
+
+extern "C" int adl_bloom_probe_server_launches(uint64_t *launches) {
+  if (!launches) return ADL_ERR_INVALID_ARG;
+  *launches = adl_srv::launches();
+  return ADL_OK;
+}

@@ -4,10 +4,17 @@
 #pragma once
 #include <stdint.h>
 
+#include <chrono>
+
 namespace adl_srv {
 
 constexpr uint32_t kMaxQ = 8;           // queries per request
 constexpr uint32_t kMaxKeyBytes = 320;  // key bytes per request
+// probe()'s answer wait before it gives up and returns kBusy (the caller then
+// probes by a launch; the request may still be served later, reading only the
+// cache arena, and its answer is ignored: each request has its own sequence)
+constexpr std::chrono::milliseconds kTimeout{200};
+constexpr int kBusy = -1000;
 
 struct Server;
 
@@ -20,9 +27,17 @@ __attribute__((visibility("hidden"))) void destroy(Server *s);
 __attribute__((visibility("hidden"))) bool eligible(uint64_t n, uint64_t key_bytes);
 // n queries (keys by offsets or fixed stride), query q against the device
 // byte range [range[2q], range[2q+1]) of k-probe filter bits; answers to
-// h_out.  Returns ADL_* status.
+// h_out.  Returns ADL_* status, or kBusy when no answer came within kTimeout.
 __attribute__((visibility("hidden"))) int probe(Server *s, const uint8_t *h_keys, const uint64_t *h_offsets,
                                                 uint32_t key_stride, uint64_t n, const uint64_t *range, uint32_t k,
                                                 uint8_t *h_out);
+
+// Servers that exist in this process (created, not destroyed): the build then
+// leaves every CU a wave slot for their kernel (bloom_build.hip, pass B).
+__attribute__((visibility("hidden"))) uint32_t live_servers();
+
+// Server kernels launched by this process so far (relaunches after the idle
+// and life limits included); readpath_test's tail-latency run reports it.
+__attribute__((visibility("hidden"))) uint64_t launches();
 
 }  // namespace adl_srv

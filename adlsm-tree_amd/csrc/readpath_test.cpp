@@ -22,6 +22,14 @@
 //     Latency of the read path: a single-key FilterBlockReader::IsKeyExists,
 //     and level multi-gets of 1k and 64k keys over 16 cached tables.  One JSON
 //     line on stdout.
+//
+//   readpath_test --tails [calls]
+//     The single-key latency distribution (p50 ... max) over many calls, across
+//     the probe server's exits and relaunches.
+//
+//   readpath_test --coexist [reps]
+//     Single-key Gets while the headline build and a configs[3]-shaped build
+//     run on another thread (Coexist below).
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -35,8 +43,12 @@
 #include <thread>
 #include <vector>
 
+#include <hip/hip_runtime_api.h>
+
+#include "adl_bloom.h"
 #include "filter_block.hpp"
 #include "level_filter.hpp"
+#include "sstable_writer.hpp"
 
 namespace {
 
@@ -176,10 +188,227 @@ int Bench() {
   return 0;
 }
 
+
+// ---------------------------------------------------------------- tails
+double Pct(std::vector<double> v, double p) {
+  if (v.empty()) return 0;
+  std::sort(v.begin(), v.end());
+  return v[std::min(v.size() - 1, (size_t)(p * (double)v.size()))];
+}
+
+void PrintLat(const char *name, const std::vector<double> &lat) {
+  printf("\"%s\": {\"calls\": %zu, \"p50\": %.2f, \"p90\": %.2f, \"p99\": %.2f, \"p99_9\": %.2f, \"max\": %.2f}", name,
+         lat.size(), Pct(lat, 0.5), Pct(lat, 0.9), Pct(lat, 0.99), Pct(lat, 0.999),
+         lat.empty() ? 0.0 : *std::max_element(lat.begin(), lat.end()));
+}
+
+// Single-key IsKeyExists through the resident probe server, `calls` times in a
+// row: the latency distribution across the server's idle / life-limit exits
+// and relaunches (each relaunch is counted).
+int Tails(size_t calls) {
+  RC rc;
+  Level lv = BuildLevel(4, 50000, 200000, &rc);
+  if (rc) return 1;
+  FilterCache cache(1ull << 28, 64, kBpk);
+  if (cache.status()) return 1;
+  FilterBlockReader reader;
+  if (cache.Put(lv.tables[0].oid, lv.blocks[0]) || reader.Init(lv.blocks[0], cache, lv.tables[0].oid)) return 1;
+  const std::vector<std::string> q = Queries(4096, 200000, 7);
+  std::vector<uint8_t> want(q.size());
+  for (size_t i = 0; i < q.size(); ++i) want[i] = reader.IsKeyExists(0, q[i]);
+  uint64_t l0 = 0, l1 = 0;
+  if (adl_bloom_probe_server_launches(&l0)) return 1;
+  std::vector<double> lat, lat_relaunch, lat_plain;
+  lat.reserve(calls);
+  size_t bad = 0;
+  const double t_start = Now();
+  uint64_t la = l0, lb = l0;
+  for (size_t i = 0; i < calls; ++i) {
+    const size_t j = i % q.size();
+    const double t0 = Now();
+    const bool hit = reader.IsKeyExists(0, q[j]);
+    const double us = (Now() - t0) * 1e6;
+    lat.push_back(us);
+    (void)adl_bloom_probe_server_launches(&lb);
+    (lb != la ? lat_relaunch : lat_plain).push_back(us);
+    la = lb;
+    bad += hit != (want[j] != 0);
+    if (i % 2000 == 1999)
+      fprintf(stderr, "tails: %zu calls, %.3f s, %llu launches\n", i + 1, Now() - t_start,
+              (unsigned long long)(lb - l0));
+  }
+  const double elapsed = Now() - t_start;
+  if (adl_bloom_probe_server_launches(&l1)) return 1;
+  std::vector<double> top = lat;
+  std::sort(top.rbegin(), top.rend());
+  top.resize(std::min<size_t>(top.size(), 12));
+  size_t over30 = 0;
+  for (double v : lat) over30 += v > 30.0;
+  printf("{");
+  PrintLat("single_key_us", lat);
+  printf(", ");
+  PrintLat("calls_that_relaunched_us", lat_relaunch);
+  printf(", ");
+  PrintLat("other_calls_us", lat_plain);
+  printf(", \"over_30us\": %zu, \"top_us\": [", over30);
+  for (size_t i = 0; i < top.size(); ++i) printf("%s%.1f", i ? ", " : "", top[i]);
+  printf("], \"elapsed_s\": %.3f, \"server_launches\": %llu, \"mismatches\": %zu}\n", elapsed,
+         (unsigned long long)(l1 - l0), bad);
+  fflush(stdout);
+  fprintf(stderr, "tails: printed, tearing down\n");
+  return bad ? 1 : 0;
+}
+
+// ---------------------------------------------------------------- coexist
+// Reads beside builds (the reference's DB::Get probes filters with no lock
+// while DoCompaction builds on the worker thread, src/db.cpp:164-172, 263,
+// 294): one thread issues single-key IsKeyExists through the resident probe
+// server while another runs the headline build (10 M 16-byte keys, one
+// filter) and a configs[3]-shaped segmented build (256 tables x 1 M keys)
+// back to back on its own stream.  Phases: builds alone, Gets alone, both.
+// Prints one JSON line: build times and Get latencies idle and concurrent,
+// the headline bitmap's SHA-256 and the SHA-256 of the 256 tables' SHA-256
+// hex digests (idle and concurrent), and the Get mismatches.
+struct DevBuf {
+  void *p = nullptr;
+  explicit DevBuf(size_t n) {
+    if (hipMalloc(&p, n) != hipSuccess) p = nullptr;
+  }
+  ~DevBuf() {
+    if (p) (void)hipFree(p);
+  }
+  uint8_t *u8() const { return static_cast<uint8_t *>(p); }
+};
+
+std::string ShaHex(const void *data, size_t n) {
+  Sha256 h;
+  h.Update(data, n);
+  unsigned char d[32];
+  h.Final(d);
+  return Sha256Hex(d);
+}
+
+int Coexist(int reps) {
+  RC rc;
+  Level lv = BuildLevel(4, 50000, 200000, &rc);
+  if (rc) return 1;
+  FilterCache cache(1ull << 28, 64, kBpk);
+  if (cache.status()) return 1;
+  FilterBlockReader reader;
+  if (cache.Put(lv.tables[0].oid, lv.blocks[0]) || reader.Init(lv.blocks[0], cache, lv.tables[0].oid)) return 1;
+  const std::vector<std::string> q = Queries(4096, 200000, 7);
+  std::vector<uint8_t> want(q.size());
+  for (size_t i = 0; i < q.size(); ++i) want[i] = reader.IsKeyExists(0, q[i]);
+
+  // build inputs, all device-resident (SURVEY §8d SplitMix keys)
+  const uint64_t n1 = 10000000, T = 256, nt = 1000000;
+  hipStream_t st;
+  if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return 1;
+  DevBuf k1(n1 * 16), b1(adl_bloom_bitmap_alloc_bytes(n1, kBpk));
+  const uint64_t ws1 = adl_bloom_build_workspace_bytes(&n1, 1, kBpk);
+  std::vector<uint64_t> counts(T, nt), kb(T + 1), boff(T);
+  for (uint64_t t = 0; t <= T; ++t) kb[t] = t * nt;
+  const uint64_t tb = adl_bloom_bitmap_bytes(nt, kBpk), tba = adl_bloom_bitmap_alloc_bytes(nt, kBpk);
+  for (uint64_t t = 0; t < T; ++t) boff[t] = t * tba;
+  const uint64_t wsc = adl_bloom_build_workspace_bytes(counts.data(), (uint32_t)T, kBpk);
+  DevBuf kc(T * nt * 16), bc(T * tba), ws(std::max(ws1, wsc));
+  if (!k1.p || !b1.p || !kc.p || !bc.p || !ws.p) return 1;
+  if (adl_synth_keys16_device(k1.u8(), 0x5EED, 0, n1, st)) return 1;
+  for (uint64_t t = 0; t < T; ++t)
+    if (adl_synth_keys16_device(kc.u8() + t * nt * 16, 0x5EED + t, 0, nt, st)) return 1;
+  hipEvent_t e0, e1;
+  if (hipEventCreate(&e0) || hipEventCreate(&e1) || hipStreamSynchronize(st)) return 1;
+  // one build; its pass A / pass B kernel times from their dispatch packets
+  // (adl_bloom_profile_*) go to pa / pb
+  auto build_ms = [&](bool headline, std::vector<double> &pa, std::vector<double> &pb) -> double {
+    if (adl_bloom_profile_enable(4) || hipEventRecord(e0, st)) return -1;
+    const int s = headline ? adl_bloom_build_device(k1.u8(), nullptr, n1, 16, kBpk, b1.u8(), ws.p, ws1, st)
+                           : adl_bloom_build_segmented_device(kc.u8(), nullptr, 16, kb.data(), (uint32_t)T, kBpk,
+                                                              bc.u8(), boff.data(), ws.p, wsc, st);
+    float ms = 0;
+    if (s || hipEventRecord(e1, st) || hipEventSynchronize(e1) || hipEventElapsedTime(&ms, e0, e1)) return -1;
+    double ab[2] = {0, 0};
+    uint32_t builds = 0;
+    if (adl_bloom_profile_collect(ab, &builds) || builds != 1) return -1;
+    pa.push_back(ab[0]);
+    pb.push_back(ab[1]);
+    return ms;
+  };
+  auto shas = [&](std::string &h1, std::string &hc) -> bool {
+    std::vector<uint8_t> h(std::max(adl_bloom_bitmap_bytes(n1, kBpk), T * tba));
+    if (hipMemcpy(h.data(), b1.p, adl_bloom_bitmap_bytes(n1, kBpk), hipMemcpyDeviceToHost)) return false;
+    h1 = ShaHex(h.data(), adl_bloom_bitmap_bytes(n1, kBpk));
+    if (hipMemcpy(h.data(), bc.p, T * tba, hipMemcpyDeviceToHost)) return false;
+    std::string cat;
+    for (uint64_t t = 0; t < T; ++t) cat += ShaHex(h.data() + boff[t], tb);
+    hc = ShaHex(cat.data(), cat.size());
+    return true;
+  };
+  std::vector<double> idle_h, idle_c, conc_h, conc_c;
+  std::vector<double> pa_h[2], pb_h[2], pa_c[2], pb_c[2];  // [idle, with Gets]
+  // phase 1: builds alone (one warm-up pair)
+  for (int r = 0; r <= reps; ++r) {
+    const double a = build_ms(true, pa_h[0], pb_h[0]), b = build_ms(false, pa_c[0], pb_c[0]);
+    if (a < 0 || b < 0) return 1;
+    if (r) idle_h.push_back(a), idle_c.push_back(b);
+  }
+  std::string sha1_idle, shac_idle, sha1_conc, shac_conc;
+  if (!shas(sha1_idle, shac_idle)) return 1;
+  // phase 2: Gets alone
+  std::vector<double> get_idle, get_conc;
+  size_t bad = 0;
+  auto one_get = [&](size_t i, std::vector<double> &lat) {
+    const size_t j = i % q.size();
+    const double t0 = Now();
+    const bool hit = reader.IsKeyExists(0, q[j]);
+    lat.push_back((Now() - t0) * 1e6);
+    bad += hit != (want[j] != 0);
+  };
+  for (size_t i = 0; i < 50000; ++i) one_get(i, get_idle);
+  // phase 3: both
+  std::atomic<bool> building{true};
+  std::atomic<int> build_fail{0};
+  std::thread builder([&] {
+    for (int r = 0; r < reps; ++r) {
+      const double a = build_ms(true, pa_h[1], pb_h[1]), b = build_ms(false, pa_c[1], pb_c[1]);
+      if (a < 0 || b < 0) ++build_fail;
+      conc_h.push_back(a);
+      conc_c.push_back(b);
+    }
+    building = false;
+  });
+  for (size_t i = 0; building.load(); ++i) one_get(i, get_conc);
+  builder.join();
+  if (build_fail || !shas(sha1_conc, shac_conc)) return 1;
+  uint64_t launches = 0;
+  (void)adl_bloom_probe_server_launches(&launches);
+  printf("{\"reps\": %d, \"build_ms\": {\"headline_idle\": %.4f, \"headline_with_gets\": %.4f, "
+         "\"compaction_idle\": %.4f, \"compaction_with_gets\": %.4f}, ",
+         reps, Pct(idle_h, 0.5), Pct(conc_h, 0.5), Pct(idle_c, 0.5), Pct(conc_c, 0.5));
+  printf("\"pass_ms\": {\"headline_a\": [%.4f, %.4f], \"headline_b\": [%.4f, %.4f], \"compaction_a\": [%.4f, %.4f], "
+         "\"compaction_b\": [%.4f, %.4f]}, ",
+         Pct(pa_h[0], 0.5), Pct(pa_h[1], 0.5), Pct(pb_h[0], 0.5), Pct(pb_h[1], 0.5), Pct(pa_c[0], 0.5),
+         Pct(pa_c[1], 0.5), Pct(pb_c[0], 0.5), Pct(pb_c[1], 0.5));
+  PrintLat("get_us_idle", get_idle);
+  printf(", ");
+  PrintLat("get_us_during_builds", get_conc);
+  printf(", \"get_mismatches\": %zu, \"headline_sha256\": [\"%s\", \"%s\"], \"compaction_sha_of_shas\": [\"%s\", \"%s\"], "
+         "\"server_launches\": %llu}\n",
+         bad, sha1_idle.c_str(), sha1_conc.c_str(), shac_idle.c_str(), shac_conc.c_str(),
+         (unsigned long long)launches);
+  return bad ? 1 : 0;
+}
+
 }  // namespace
 
 int main(int argc, char **argv) {
   if (argc > 1 && strcmp(argv[1], "--bench") == 0) return Bench();
+  if (argc > 1 && strcmp(argv[1], "--tails") == 0) {
+    const int rc = Tails(argc > 2 ? (size_t)atoll(argv[2]) : 200000);
+    fprintf(stderr, "tails: returned %d\n", rc);
+    return rc;
+  }
+  if (argc > 1 && strcmp(argv[1], "--coexist") == 0) return Coexist(argc > 2 ? atoi(argv[2]) : 5);
   if (argc < 2) {
     fprintf(stderr, "usage: readpath_test <outdir> [threads] [rounds] | --bench\n");
     return 2;

@@ -2,7 +2,9 @@
 // test/sstable_test.cpp (BuildSSTable :9-27, BuildSSTable2 :29-43) flushed
 // through the gfx950-backed SSTableWriter (sstable_writer.hpp).  Needs a GPU.
 //
-//   sstable_test <which 1|2> <dir>   writes <dir>/<oid>.sst, prints "<oid> <bytes>"
+//   sstable_test <which 1|2|3> <dir> writes <dir>/<oid>.sst, prints "<oid> <bytes> <dups>"
+//                                    (3: 1-5 versions per user key; dups = the filter keys
+//                                    equal to their predecessor, skipped on the device)
 //   sstable_test batch <which> <dir> the same through AddBatch (packed run)
 //   sstable_test sha256 <file>       the writer's SHA-256 of a file (CPU only)
 //   sstable_test bench <n> <dir>     flush an n-entry memtable ("key%012d" / 100-byte
@@ -58,7 +60,15 @@ std::string InnerKey(const Entry &e) {
 
 std::vector<Entry> Memtable(int which) {
   std::vector<Entry> v;
-  for (int i = 0; i < 10000; ++i) {
+  if (which == 3) {
+    // 1-5 versions of each of 4 000 user keys (puts and deletes): in memtable
+    // order a user key's versions are adjacent filter keys
+    int64_t seq = 0;
+    for (int j = 0; j < 4000; ++j)
+      for (int r = 0; r <= (j * 7) % 5; ++r, ++seq)
+        v.push_back({"user" + std::to_string(j), seq, seq % 3 == 2 ? 1 : 0, "v" + std::to_string(seq)});
+  }
+  for (int i = 0; which != 3 && i < 10000; ++i) {
     if (which == 1)
       v.push_back({"key" + std::to_string(i), i, 0, "value" + std::to_string(i)});
     else
@@ -206,7 +216,7 @@ int main(int argc, char **argv) {
     return 2;
   }
   const int which = atoi(argv[a]);
-  if (which != 1 && which != 2) return 2;
+  if (which < 1 || which > 3) return 2;
   const auto mem = Memtable(which);
 
   PosixFileSink sink(argv[a + 1]);
@@ -231,11 +241,12 @@ int main(int argc, char **argv) {
       if ((rc = w.Add(InnerKey(e), e.value))) break;
   }
   unsigned char digest[32];
+  const unsigned long long dups = w.filter_duplicates();
   if (!rc) rc = w.Final(digest);
   if (rc) {
     fprintf(stderr, "sstable build failed: %s\n", std::string(strrc(rc)).c_str());
     return 1;
   }
-  printf("%s %d\n", Sha256Hex(digest).c_str(), w.GetFileSize());
+  printf("%s %d %llu\n", Sha256Hex(digest).c_str(), w.GetFileSize(), dups);
   return 0;
 }

@@ -159,6 +159,12 @@ SSTableWriter::SSTableWriter(Sink *sink, int bits_per_key)
 SSTableWriter::SSTableWriter(Sink *sink, unique_ptr<FilterAlgorithm> &&filter)
     : sink_(sink), filter_block_(std::move(filter)) {}
 
+/* a build BeginFinal posted writes filter_block_ and filter_out_: it must end
+ * before they do (an error path that drops a writer between the halves) */
+SSTableWriter::~SSTableWriter() {
+  if (filter_job_.valid()) filter_job_.wait();
+}
+
 /* src/sstable.cpp:26-35: the user key (inner key minus seq and op,
  * src/keys.cpp:7-9) goes to the filter, the entry to the data block. */
 RC SSTableWriter::Add(string_view inner_key, string_view value) {
@@ -174,8 +180,11 @@ RC SSTableWriter::Add(string_view inner_key, string_view value) {
 /* A packed sorted run (memtable flush, src/mem_table.cpp:96-105; MergeRuns
  * output, src/db.cpp:428-509): the user keys go into the filter arena in one
  * bulk append (one reservation, no per-entry call), then the entries into the
- * data blocks.  Same bytes as Add() per entry; every record is checked before
- * anything is added, so a BAD_RECORD leaves the writer unchanged. */
+ * data blocks.  Same bytes as Add() per entry.  Every record is checked before
+ * anything is added, so a BAD_RECORD leaves the writer unchanged; an error
+ * from the sink while a data block is flushed does not (the filter then holds
+ * keys of entries that were not written), and the table must be abandoned, as
+ * after any failed Add. */
 RC SSTableWriter::AddBatch(const char *keys, const uint64_t *key_off, const char *values,
                            const uint64_t *val_off, size_t n) {
   if (filter_job_.valid()) return BAD_RECORD;

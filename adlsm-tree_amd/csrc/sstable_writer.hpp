@@ -140,6 +140,10 @@ class SSTableWriter {
   /* any FilterAlgorithm (src/filter_block.hpp:13-20), e.g. one written
    * against the reference's interface */
   SSTableWriter(Sink *sink, unique_ptr<FilterAlgorithm> &&filter);
+  /* waits for a filter build BeginFinal started and EndFinal did not collect */
+  ~SSTableWriter();
+  SSTableWriter(const SSTableWriter &) = delete;
+  SSTableWriter &operator=(const SSTableWriter &) = delete;
   /* inner_key = user_key + LE64 seq + op byte (src/keys.cpp:76-84) */
   RC Add(string_view inner_key, string_view value);
   /* entries i = [key_off[i], key_off[i+1]) of keys, [val_off[i], val_off[i+1])
@@ -158,6 +162,9 @@ class SSTableWriter {
   RC BeginFinal();
   RC EndFinal(unsigned char sha256_digit[32]);
   int GetFileSize() const { return offset_; }
+  /* filter keys added so far that equal their predecessor (user keys of
+   * consecutive versions); Final skips them on the device when frequent */
+  uint64_t filter_duplicates() const { return filter_block_.adjacent_duplicates(); }
   /* wall time of the filter block build of the last Final() / EndFinal();
    * not valid between BeginFinal and EndFinal */
   double filter_seconds() const { return filter_seconds_; }
@@ -177,8 +184,10 @@ class SSTableWriter {
   string last_key_;
   string buffer_;
   double filter_seconds_ = 0;
-  /* BeginFinal's build and its block (declared in this order so the future,
-   * whose destructor waits for the build, goes first) */
+  /* BeginFinal's build and the block it writes.  The future comes from a
+   * packaged_task on the filter worker, so its destructor does not wait:
+   * ~SSTableWriter waits for a pending build, which uses filter_block_ and
+   * filter_out_. */
   string filter_out_;
   future<FilterOutcome> filter_job_;
   static constexpr size_t need_flush_size_ = 1u << 12; /* 4KB, src/sstable.hpp:40 */

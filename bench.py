@@ -152,6 +152,7 @@ class Workload:
         if queries % world:
             raise SystemExit(f"--queries {queries} must divide over {world} ranks")
         self.gidx = None  # batch positions of this rank's queries (owner-bucketed, N > 1)
+        self.bucketing_ms = None
         if world == 1:
             self.n = queries
             self.keys, self.fid, self.member = ab.synth_probe_queries(queries, num_tables=PROBE_TABLES,
@@ -159,7 +160,11 @@ class Workload:
         else:
             # owner-bucketed: the whole batch, bucketed by owner before
             # upload -- this rank keeps exactly its own tables' queries, batch order kept;
-            # self.fid holds filter ids local to this rank
+            # self.fid holds filter ids local to this rank.  Its cost (outside the timed
+            # loop: a lookup is issued where its level's tables live) is reported as
+            # probe_bucketing_ms.
+            torch.cuda.synchronize()
+            tb0 = time.perf_counter()
             ks, fs, ms, ix = [], [], [], []
             chunk = 8_000_000
             for q0 in range(0, queries, chunk):
@@ -173,6 +178,8 @@ class Workload:
                 del k, f, m
             self.keys, self.fid, self.member, self.gidx = (torch.cat(ks), torch.cat(fs), torch.cat(ms),
                                                            torch.cat(ix))
+            torch.cuda.synchronize()
+            self.bucketing_ms = (time.perf_counter() - tb0) * 1e3
             self.n = int(self.keys.shape[0])
             # the routed variant's input: this rank's contiguous slice of the batch
             rq0, rn = rank * (queries // world), queries // world
@@ -631,6 +638,28 @@ def alu_roofline(workload, n_keys, kernels_us):
     return out
 
 
+def lds_roofline(workload, kernels_us):
+    """roofline.lds from the committed PMC pass (tools/pmc_lds.py): per build
+    pass, the LDS array's cycles and the share of them spent in bank
+    conflicts, as a busy fraction of this run's kernel time, and the array
+    time with and without the conflict cycles (the floor an LDS-bound pass
+    could reach, MI355X_MICROARCH.md §LDS)."""
+    e = load_pmc(workload).get("lds")
+    if not e:
+        return None
+    out = {"source": "profiles/pmc_traffic.json (SQ_LDS_IDX_ACTIVE, SQ_LDS_BANK_CONFLICT, GRBM_GUI_ACTIVE)",
+           "model": "array cycles summed over 256 CUs; busy = cycles / (256 x kernel cycles)"}
+    for k, v in e.items():
+        us = kernels_us.get(k)
+        clk = v.get("clock_ghz") or 2.4
+        arr_us = v["array_cycles"] / 256 / (clk * 1e3)
+        out[k] = {"conflict_frac": v.get("conflict_frac"), "clock_ghz": clk,
+                  "array_us": round(arr_us, 2),
+                  "array_us_without_conflicts": round((v["array_cycles"] - v["conflict_cycles"]) / 256 / (clk * 1e3), 2),
+                  "array_busy_frac": round(arr_us / us, 4) if us else None}
+    return out
+
+
 def main():
     args = parse()
     import torch
@@ -646,8 +675,11 @@ def main():
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs a GPU")
     torch.cuda.set_device(local)
+    backend = None
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        world = dist.get_world_size()
+        backend = dist.get_backend()
 
     def barrier():
         torch.cuda.synchronize()
@@ -735,6 +767,9 @@ def main():
                        "ms_per_step": round(el / max(args.steps, 1) * 1e3, 4), "steps": args.steps,
                        "scaling": "strong", "tables_total": COMPACTION_TABLES, "tables_per_gpu": len(wc.tables),
                        "parity": build_parity(wc, rank)}
+        if rank == 0 and not args.no_cpu_baseline:
+            # every N: the reference's filter builds on this host's cores for the same tables
+            comp_strong["cpu_baseline"] = cpu_baseline(min(args.cpu_seconds, 5.0), "compaction", wc)
         del wc
         torch.cuda.empty_cache()
 
@@ -766,6 +801,8 @@ def main():
         stream_gbs = hbm_stream_read_gbs()
         if probe:
             metric = "Mqueries/s bloom-filter probe (device-resident), 16B keys, 256 filters, bits/key=10"
+            if world > 1:
+                metric += ", owner-bucketed"
         elif args.workload == "varlen":
             metric = "Mkeys/s bloom-filter build (device-resident), var-len keys, bits/key=10"
         else:
@@ -785,6 +822,7 @@ def main():
             "dtype": w.dtype,
             "data": "synthetic (SplitMix64 keys generated on device, SURVEY.md §8d)",
             "config": dict(w.config, parallelism=f"whole filters per GPU x{world}, no data-path collective"),
+            "world": {"size": world, "backend": backend or "none (one process)"},
             "roofline": {
                 "bound": "hbm",
                 "achieved": round(achieved, 1) if achieved else None,
@@ -821,8 +859,11 @@ def main():
             }
         if traffic and timed:
             out_json["roofline"]["traffic_gbs"] = round(traffic / (kern_ms * 1e-3) / 1e9, 1)
+        if probe and w.bucketing_ms is not None:
+            out_json["probe_bucketing_ms"] = round(w.bucketing_ms, 2)
         if not probe:
             out_json["roofline"]["alu"] = alu_roofline(args.workload, w.n, kernels)
+            out_json["roofline"]["lds"] = lds_roofline(args.workload, kernels)
             pos = w.builder.positions()
             out_json["roofline"]["positions_per_build"] = {
                 "positions": pos, "per_key": round(pos / w.n, 3),

@@ -140,6 +140,14 @@ int adl_bloom_build_segmented(const uint8_t *h_keys, const uint64_t *h_offsets, 
                               const uint64_t *key_begin, uint32_t num_filters, int32_t bits_per_key,
                               uint8_t *h_bitmaps, const uint64_t *h_bitmap_off, void *stream);
 
+/* adl_bloom_build_segmented with flags (ADL_BLOOM_SKIP_ADJACENT_DUPLICATES; 0 =
+ * identical to it): the host side of SSTableWriter::Final (src/sstable.cpp:58),
+ * whose filters hold the user keys of a memtable run, versions of one user key
+ * in a row (src/sstable.cpp:28, src/keys.cpp:61-74). */
+int adl_bloom_build_segmented_ex(const uint8_t *h_keys, const uint64_t *h_offsets, uint32_t key_stride,
+                                 const uint64_t *key_begin, uint32_t num_filters, int32_t bits_per_key,
+                                 uint8_t *h_bitmaps, const uint64_t *h_bitmap_off, uint32_t flags, void *stream);
+
 /* ------------------------------------------------- filter block on the device */
 
 /* Size of the filter block FilterBlockWriter::Final (src/filter_block.cpp:77-102)
@@ -339,6 +347,17 @@ int adl_bloom_build_positions(const uint64_t *key_counts, uint32_t num_filters, 
 #define ADL_TEST_FAULT_PIPELINE_GROUP 1
 #define ADL_TEST_FAULT_CACHE_COMPLETION 2
 int adl_bloom_test_fault(int site, int64_t arg);
+
+/* The tuning and test switches (ADL_BLOOM_* environment variables, DESIGN.md
+ * §8) are read once per process, at the first call that needs them.  This
+ * reads them again (tests that change them; no other call of the library may
+ * be running). */
+int adl_bloom_reload_knobs(void);
+
+/* Resident probe server kernels launched by this process so far (first
+ * launches and relaunches after an idle or life-limit exit), for the latency
+ * tests (readpath_test --tails). */
+int adl_bloom_probe_server_launches(uint64_t *launches);
 
 /* ---------------------------------------------------------------- synthetic data */
 

@@ -137,7 +137,8 @@ def oid(file_bytes: bytes) -> str:
 
 def sstable_test_entries(which: int = 1):
     """The memtables of test/sstable_test.cpp: BuildSSTable (:9-27, which=1) and
-    BuildSSTable2 (:29-43, which=2), as sorted (inner_key, value) pairs."""
+    BuildSSTable2 (:29-43, which=2), as sorted (inner_key, value) pairs; which=3
+    is a memtable of many versions per user key."""
     ents = []
     if which == 1:
         for i in range(10000):
@@ -145,6 +146,14 @@ def sstable_test_entries(which: int = 1):
     elif which == 2:
         for i in range(10000):
             ents.append((b"key%d" % (i // 2), i, OP_PUT if i % 2 == 0 else OP_DELETE, b"value%d" % (i // 2)))
+    elif which == 3:
+        # not a reference memtable: 1-5 versions of each of 4 000 user keys
+        # (adlsm-tree_amd/csrc/sstable_test.cpp Memtable(3))
+        seq = 0
+        for j in range(4000):
+            for _r in range((j * 7) % 5 + 1):
+                ents.append((b"user%d" % j, seq, OP_DELETE if seq % 3 == 2 else OP_PUT, b"v%d" % seq))
+                seq += 1
     else:
         raise ValueError(which)
     return [(inner_key(u, s, o), v) for (u, s, o, v) in memtable_order(ents)]

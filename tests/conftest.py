@@ -32,3 +32,24 @@ def golden():
     with open(os.path.join(d, "murmur3_ref.json")) as f:
         mm = json.load(f)
     return {"appendix_b": app, "murmur3": mm}
+
+
+@pytest.fixture
+def knobs(monkeypatch):
+    """ADL_BLOOM_* switches for one test.  The library reads them once per
+    process, so every change is followed by adl_bloom_reload_knobs(), and the
+    teardown restores the environment and reloads it."""
+    import adlbloom
+
+    class Knobs:
+        def set(self, name, value):
+            monkeypatch.setenv(name, str(value))
+            adlbloom.reload_knobs()
+
+        def unset(self, name):
+            monkeypatch.delenv(name, raising=False)
+            adlbloom.reload_knobs()
+
+    yield Knobs()
+    monkeypatch.undo()
+    adlbloom.reload_knobs()

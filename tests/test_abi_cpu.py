@@ -83,17 +83,6 @@ def test_workspace_bytes():
     assert adlbloom.workspace_bytes([2**31], 10) == 0  # too large -> 0
 
 
-def test_workspace_bytes_bucketed(monkeypatch):
-    """ADL_BLOOM_BK=1 (the bucketed build): per (slice, tile) regions of the
-    expected share plus six sigma (~400 MB at 256 x 763), each slice's
-    overflow pool sized for any key distribution (~255 MB), the count tables
-    and (h1, h2) 8 B per key for variable-length keys."""
-    import adlbloom
-
-    monkeypatch.setenv("ADL_BLOOM_BK", "1")
-    assert 700_000_000 <= adlbloom.workspace_bytes([10_000_000], 10) < 760_000_000
-
-
 def test_missing_library_fails_loudly(monkeypatch, tmp_path):
     import adlbloom
 

@@ -44,25 +44,25 @@ def ab():
 
 
 @pytest.fixture(params=list(SETTINGS), ids=list(SETTINGS))
-def claim(request, monkeypatch):
+def claim(request, knobs):
     for k, v in SETTINGS[request.param].items():
-        monkeypatch.setenv(k, v)
+        knobs.set(k, v)
     return request.param
 
 
-def test_claim_plan_selected(dev, ab, monkeypatch, capfd):
+def test_claim_plan_selected(dev, ab, knobs, capfd):
     """ADL_BLOOM_CLAIM=1 takes the claim layout for 32 filters of 100 K keys
     (31 tiles of 2^18 bits each, about 800 positions per tile and chunk) and
     refuses it for the headline's single 10 M-key filter (763 tiles of 2^20
     bits, about 44 per tile and chunk: too few for a fixed share)."""
-    monkeypatch.setenv("ADL_BLOOM_CLAIM", "1")
-    monkeypatch.setenv("ADL_BLOOM_DEBUG", "1")
+    knobs.set("ADL_BLOOM_CLAIM", "1")
+    knobs.set("ADL_BLOOM_DEBUG", "1")
     assert ab.workspace_bytes([100_000] * 32, 10) > 0
     assert "(claim)" in capfd.readouterr().err
     assert ab.workspace_bytes([10_000_000], 10) > 0
     assert "(claim)" not in capfd.readouterr().err
     # default: only filters of at most 10 tiles (256 x 10 K: 4 tiles each)
-    monkeypatch.delenv("ADL_BLOOM_CLAIM")
+    knobs.unset("ADL_BLOOM_CLAIM")
     assert ab.workspace_bytes([10_000] * 256, 10) > 0
     assert "(claim)" in capfd.readouterr().err
     assert ab.workspace_bytes([100_000] * 32, 10) > 0
@@ -151,12 +151,12 @@ def test_claim_segmented_varlen_many_filters(dev, ab, oracle, claim):
         assert np.array_equal(out[int(boff[f]):int(boff[f]) + int(nbytes[f])], want), f
 
 
-def test_claim_positions_count(dev, ab, oracle, claim, monkeypatch):
+def test_claim_positions_count(dev, ab, oracle, claim, knobs):
     """adl_bloom_build_positions reads the claim layout's (start, length)
     entries: with the pair table off every key writes k = 6 positions, and
     the bitmaps still equal the oracle's (256 filters of 10 K keys, the
     default's claim shape)."""
-    monkeypatch.setenv("ADL_BLOOM_HASH_DEDUP", "0")
+    knobs.set("ADL_BLOOM_HASH_DEDUP", "0")
     sizes = [10_000] * 255 + [9_999]
     kb = np.concatenate([[0], np.cumsum(sizes)]).astype(np.uint64)
     keys = ab.synth_keys16(int(kb[-1]), seed=99)
@@ -167,3 +167,49 @@ def test_claim_positions_count(dev, ab, oracle, claim, monkeypatch):
     for f in (0, 1, 128, 255):
         o = int(sb.boff[f])
         assert np.array_equal(out[o:o + int(sb.sizes[f])], oracle.keys2block(hk[kb[f]:kb[f + 1]])), f
+
+
+def test_builds_with_a_resident_server(dev, ab, oracle, golden):
+    """While a resident probe server exists (a reader), pass A and pass B take
+    their chunks and tiles from the work queues (GroupQueue, bloom_build.hip)
+    instead of the static stripes.  The same bitmaps: the 10 M reference SHA
+    (chunk/table layout), 256 x 10 K (claim layout), 32 x 100 K (two pass-B
+    workgroups per CU), var-len keys, built while single-key Gets keep the
+    server running."""
+    blk_keys = oracle.splitmix_keys16(0x5151, 20_000)
+    bm0 = oracle.keys2block(blk_keys)
+    cache = ab.FilterCache(8 << 20, max_tables=8)
+    # a one-filter block in the reference's framing
+    cache.put(b"t0", oracle.filter_block_final([bm0.tobytes()], bits_per_key=10))
+    t = np.zeros(1, np.uint32)
+
+    def get(i):
+        got, _ = cache.probe([b"t0"], t, blk_keys[i:i + 1])
+        assert got[0] == 1  # an inserted key
+
+    try:
+        get(0)  # the server now exists
+        g = golden["appendix_b"]["bitmaps"][5]
+        keys = ab.synth_keys16(g["n"], seed=0x5EED)
+        b = ab.Builder(g["n"], 10)
+        for r in range(3):
+            get(r + 1)
+            bm = b.build(keys).cpu().numpy()
+            assert hashlib.sha256(bm.tobytes()).hexdigest() == g["sha256"], r
+        del keys, b
+        for sizes in ([10_000] * 256, [100_000] * 32, [1, 0, 70_000, 5]):
+            get(7)
+            kb = np.concatenate([[0], np.cumsum(sizes)]).astype(np.uint64)
+            hk = oracle.splitmix_keys16(0xAB + len(sizes), int(kb[-1]))
+            out, boff, nbytes = ab.build_segmented(dev.from_numpy(hk).cuda(), kb)
+            out = out.cpu().numpy()
+            for f in range(len(sizes)):
+                if sizes[f]:
+                    assert np.array_equal(out[int(boff[f]):int(boff[f]) + int(nbytes[f])],
+                                          oracle.keys2block(hk[int(kb[f]):int(kb[f + 1])])), (len(sizes), f)
+        data, offs = ab.synth_varlen(300_000, seed=5)
+        get(9)
+        got = ab.build(data, offs).cpu().numpy()
+        assert np.array_equal(got, oracle.keys2block(data.cpu().numpy(), offs.cpu().numpy().view(np.uint64)))
+    finally:
+        cache.close()

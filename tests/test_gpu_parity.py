@@ -131,75 +131,11 @@ def test_build_bits_per_key_sweep(dev, ab, oracle, bpk):
 
 
 @pytest.mark.parametrize("tl", [10, 11, 13, 15, 17, 19, 20])
-def test_build_tile_size_invariance(dev, ab, oracle, tl, monkeypatch):
-    monkeypatch.setenv("ADL_BLOOM_TILE_LOG2", str(tl))
+def test_build_tile_size_invariance(dev, ab, oracle, tl, knobs):
+    knobs.set("ADL_BLOOM_TILE_LOG2", tl)
     keys = ab.synth_keys16(150_000, seed=99)
     bm = ab.build(keys).cpu().numpy()
     assert np.array_equal(bm, oracle.keys2block(keys.cpu().numpy()))
-
-
-def test_build_atomic_path_matches(dev, ab, oracle, monkeypatch):
-    monkeypatch.setenv("ADL_BLOOM_BUILD_ALGO", "atomic")
-    for n in (0, 5, 100_000):
-        keys = ab.synth_keys16(n, seed=5)
-        b = ab.Builder(n, 10)
-        b.bitmap.fill_(0xA5)  # the build must not rely on a pre-zeroed bitmap
-        bm = b.build(keys).cpu().numpy()
-        assert np.array_equal(bm, oracle.keys2block(keys.cpu().numpy().reshape(n, 16)))
-
-
-def test_build_binned_overwrites_dirty_bitmap(dev, ab, oracle):
-    keys = ab.synth_keys16(77_777, seed=6)
-    b = ab.Builder(77_777, 10)
-    b.bitmap.fill_(0xFF)
-    b.ws.fill_(0x5A)
-    bm = b.build(keys).cpu().numpy()
-    assert np.array_equal(bm, oracle.keys2block(keys.cpu().numpy()))
-    assert not b.bitmap[b.nbytes:].any().item()  # 16-byte pad written as zero
-
-
-def test_build_duplicate_keys_hot_words(dev, ab, oracle):
-    # the collapsed-entropy hash concentrates bits; all-identical keys are the extreme
-    base = ab.synth_keys16(7, seed=1).cpu().numpy()
-    keys = np.repeat(base, 20000, axis=0)
-    bm = ab.build(to_dev(dev, keys)).cpu().numpy()
-    assert np.array_equal(bm, oracle.keys2block(keys))
-
-
-# ----------------------------------------------------------------- build, other key shapes
-@pytest.mark.parametrize("lo,hi,alpha", [(0, 40, None), (1, 300, None), (8, 8, None), (0, 3, None),
-                                         (3, 30, b"abcdefghij-0123456789")])
-def test_build_varlen_vs_oracle(dev, ab, oracle, lo, hi, alpha):
-    rng = random.Random(lo * 1000 + hi)
-    keys = rand_keys(rng, 7000, lo, hi, alpha)
-    dk, do, data, offs = packed_dev(dev, keys)
-    bm = ab.build(dk, do).cpu().numpy()
-    assert np.array_equal(bm, oracle.keys2block(data, offs))
-
-
-def test_build_synth_zipf_varlen(dev, ab, oracle):
-    data, offs = ab.synth_varlen(200_000, seed=0x5EED)
-    lens = (offs[1:] - offs[:-1]).cpu().numpy()
-    assert lens.min() >= 8 and lens.max() <= 256
-    assert 30 < lens.mean() < 50  # Zipf(1.1) over 8..256: mean ~40 B
-    bm = ab.build(data, offs).cpu().numpy()
-    h_off = offs.cpu().numpy().view(np.uint64)
-    assert np.array_equal(bm, oracle.keys2block(data.cpu().numpy(), h_off))
-
-
-def test_build_varlen_long_and_mixed_keys(dev, ab, oracle):
-    # the length-sorted hashing pass: keys of 0..3000 bytes (several load windows
-    # per key, the longer-than-510 bin), a run of 70 equal 511-byte keys, bytes
-    # >= 0x80, and a buffer that ends exactly at the last key (its lanes hash
-    # bytewise instead of reading past the end)
-    rng = random.Random(31)
-    keys = [rng.randbytes(rng.randrange(0, 3001)) for _ in range(3000)]
-    keys += [b"x" * 511] * 70 + [bytes([0x80 + i % 100]) * (i % 41) for i in range(200)]
-    rng.shuffle(keys)
-    data, offs = oracle.pack(keys)
-    data = data[: int(offs[-1])]
-    bm = ab.build(to_dev(dev, data), to_dev(dev, offs.view(np.int64))).cpu().numpy()
-    assert np.array_equal(bm, oracle.keys2block(data, offs))
 
 
 def test_build_varlen_all_empty_keys(dev, ab, oracle):
@@ -210,34 +146,27 @@ def test_build_varlen_all_empty_keys(dev, ab, oracle):
     assert np.array_equal(bm, oracle.keys2block(data, offs))
 
 
-@pytest.mark.parametrize("var_hash", ["0", "1"])
-def test_build_varlen_hash_pass_switch(dev, ab, oracle, monkeypatch, var_hash):
-    # ADL_BLOOM_VAR_HASH=0 is the fused pass A that hashes inside the chunk loop
-    monkeypatch.setenv("ADL_BLOOM_VAR_HASH", var_hash)
+@pytest.mark.parametrize("shift", [0, 1])
+def test_build_varlen_aligned_and_unaligned(dev, ab, oracle, shift):
+    """A 16-byte-aligned key buffer takes the length-sorted hashing pass and
+    pass A over (h1, h2); an unaligned one (shift 1) the fused pass A, which
+    hashes inside its chunk loop from global memory."""
     data, offs = ab.synth_varlen(120_000, seed=77)
-    bm = ab.build(data, offs).cpu().numpy()
+    if shift:
+        buf = dev.empty(data.numel() + 32, dtype=dev.uint8, device=data.device)
+        buf[shift:shift + data.numel()] = data
+        kd = buf[shift:shift + data.numel()]
+        assert kd.data_ptr() % 16 == shift
+    else:
+        kd = data
+    bm = ab.build(kd, offs).cpu().numpy()
     assert np.array_equal(bm, oracle.keys2block(data.cpu().numpy(), offs.cpu().numpy().view(np.uint64)))
 
 
-@pytest.mark.parametrize("hv_keys", ["256", "1024", "2048"])
-def test_build_varlen_hashing_run_sizes(dev, ab, oracle, monkeypatch, hv_keys):
-    # the hashing pass's other run sizes (ADL_BLOOM_HV_KEYS; 512 is the default)
-    monkeypatch.setenv("ADL_BLOOM_HV_KEYS", hv_keys)
-    data, offs = ab.synth_varlen(150_001, seed=int(hv_keys))
-    bm = ab.build(data, offs).cpu().numpy()
-    assert np.array_equal(bm, oracle.keys2block(data.cpu().numpy(), offs.cpu().numpy().view(np.uint64)))
-
-
-@pytest.mark.parametrize("split", ["0", "1", "2"])
-def test_build_varlen_seed_split(dev, ab, oracle, monkeypatch, split):
-    """ADL_BLOOM_HV_SPLIT: a hashing run's longest groups hashed by two waves,
-    one seed each (hash_lds1), the rest as before; runs with fewer groups than
-    the split (short filters), keys past the staged bytes and long keys."""
-    monkeypatch.setenv("ADL_BLOOM_HV_SPLIT", split)
-    data, offs = ab.synth_varlen(150_001, seed=91 + int(split))
-    bm = ab.build(data, offs).cpu().numpy()
-    assert np.array_equal(bm, oracle.keys2block(data.cpu().numpy(), offs.cpu().numpy().view(np.uint64)))
-    rng = np.random.default_rng(int(split))
+def test_build_varlen_run_shapes(dev, ab, oracle):
+    """Hashing runs with fewer groups than waves (short filters), keys past the
+    staged bytes and long keys."""
+    rng = np.random.default_rng(3)
     for n, lo, hi in ((1, 0, 40), (70, 0, 300), (1000, 200, 700), (5000, 0, 90)):
         lens = rng.integers(lo, hi + 1, n)
         o = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
@@ -246,11 +175,9 @@ def test_build_varlen_seed_split(dev, ab, oracle, monkeypatch, split):
         assert np.array_equal(got, oracle.keys2block(kb, o)), (n, lo, hi)
 
 
-@pytest.mark.parametrize("mode", ["1", "2"])
-def test_build_pair_table_modes(dev, ab, oracle, monkeypatch, mode):
-    # ADL_BLOOM_DD_MODE 1: every key claims its (h1, h2); 2 (default): keys with
-    # h1 == h2 claim h1.  1.5M SplitMix keys: 269 chunks, more than one round
-    monkeypatch.setenv("ADL_BLOOM_DD_MODE", mode)
+def test_build_pair_table_many_rounds(dev, ab, oracle):
+    # pass A's repeated-hash table (keys with h1 == h2 claim h1) over 1.5M
+    # SplitMix keys: 269 chunks, more than one round of the grid
     keys = ab.synth_keys16(1_500_000, seed=0x5EED)
     bm = ab.build(keys).cpu().numpy()
     assert np.array_equal(bm, oracle.keys2block(keys.cpu().numpy()))
@@ -304,12 +231,12 @@ def test_build_segmented_vs_oracle(dev, ab, oracle):
 
 
 @pytest.mark.parametrize("dedup", ["0", "1"])
-def test_build_segmented_same_keys_every_filter(dev, ab, oracle, monkeypatch, dedup):
+def test_build_segmented_same_keys_every_filter(dev, ab, oracle, knobs, dedup):
     # pass A skips a key whose hash pair its workgroup already counted; the pair
     # table must start over at a filter boundary (positions depend on m), so
     # filters holding the same keys each get every bit.  4 x 500k keys = 360
     # chunks > one grid round, so workgroups cross filters.
-    monkeypatch.setenv("ADL_BLOOM_HASH_DEDUP", dedup)
+    knobs.set("ADL_BLOOM_HASH_DEDUP", dedup)
     n = 500_000
     base = ab.synth_keys16(n, seed=0xD0D0)
     keys = dev.cat([base, base, base[: n // 2], base])
@@ -344,48 +271,6 @@ def test_build_compaction_shape_32_tables(dev, ab, oracle):
     out, boff, nbytes = ab.build_segmented(keys, kb)
     out = out.cpu().numpy()
     for t in (0, 1, 17, 31):
-        got = out[int(boff[t]):int(boff[t]) + int(nbytes[t])]
-        assert np.array_equal(got, oracle.keys2block(oracle.splitmix_keys16(0x5EED + t, n))), t
-
-
-@pytest.mark.parametrize("compact", ["0", "1"])
-def test_build_collapsed_keys_stamped(dev, ab, oracle, golden, monkeypatch, compact):
-    """ADL_BLOOM_HOT=1 (opt-in, round 4): a 16-byte key whose murmur seeds
-    collapse marks its index (one of 4 096) per workgroup and filter instead of
-    binning k positions, and pass B adds the marked indices' bits; with
-    ADL_BLOOM_COMPACT=1 the live keys are also staged densely in LDS.  The
-    10 M reference SHA (7 chunks per workgroup, three builds into the same
-    workspace: each launch pair's stamps carry a new nonce), 1.5 M keys, a
-    segmented build mixing filters of only collapsed keys with ordinary and
-    empty ones, and the 32-table shape (several filters per workgroup)."""
-    monkeypatch.setenv("ADL_BLOOM_HOT", "1")
-    monkeypatch.setenv("ADL_BLOOM_COMPACT", compact)
-    g = golden["appendix_b"]["bitmaps"][5]
-    keys = ab.synth_keys16(g["n"], seed=0x5EED)
-    b = ab.Builder(g["n"], 10)
-    for _ in range(3):
-        bm = b.build(keys).cpu().numpy()
-        assert hashlib.sha256(bm.tobytes()).hexdigest() == g["sha256"]
-    k15 = ab.synth_keys16(1_500_000, seed=0x5EED)
-    assert np.array_equal(ab.build(k15).cpu().numpy(), oracle.keys2block(k15.cpu().numpy()))
-    # filters of collapsed keys only (h1 == h2), ordinary ones and empty ones in one build
-    pool = oracle.splitmix_keys16(0xC011, 400_000)
-    hh = oracle.murmur3_batch(pool)
-    hot = pool[hh[:, 0] == hh[:, 1]]
-    plain = oracle.splitmix_keys16(0xC012, 120_000)
-    parts = [hot[:50_000], plain[:100_000], hot[50_000:50_007], plain[100_000:100_001], hot[:0], hot[60_000:]]
-    kb = np.concatenate([[0], np.cumsum([len(x) for x in parts])]).astype(np.uint64)
-    out, boff, nbytes = ab.build_segmented(dev.from_numpy(np.concatenate(parts)).cuda(), kb)
-    out = out.cpu().numpy()
-    for f, x in enumerate(parts):
-        got = out[int(boff[f]):int(boff[f]) + int(nbytes[f])]
-        if len(x):
-            assert np.array_equal(got, oracle.keys2block(x)), f
-    T, n = 32, 100_000
-    kt = dev.cat([ab.synth_keys16(n, seed=0x5EED + t) for t in range(T)])
-    out, boff, nbytes = ab.build_segmented(kt, np.arange(T + 1, dtype=np.uint64) * n)
-    out = out.cpu().numpy()
-    for t in (0, 5, 31):
         got = out[int(boff[t]):int(boff[t]) + int(nbytes[t])]
         assert np.array_equal(got, oracle.keys2block(oracle.splitmix_keys16(0x5EED + t, n))), t
 
@@ -428,14 +313,11 @@ def test_build_segmented_host_varlen(dev, ab, oracle):
         assert np.array_equal(out[int(boff[f]):int(boff[f]) + nbytes[f]], want), f
 
 
-@pytest.mark.parametrize("bk", ["0", "1"])
-def test_build_segmented_varlen_many_filters(dev, ab, oracle, monkeypatch, bk):
+def test_build_segmented_varlen_many_filters(dev, ab, oracle):
     """More than 8 variable-length filters in one launch (the descriptor-table
     path of the hashing pass, its run -> filter map, and of pass A/B): empty and
     1-key filters, filters of 511 / 512 / 513 / 1025 keys around the 512-key
-    hashing runs, through the device and the pipelined host entry points.
-    ADL_BLOOM_BK=0 is the chunk/table build, 1 the bucketed build."""
-    monkeypatch.setenv("ADL_BLOOM_BK", bk)
+    hashing runs, through the device and the pipelined host entry points."""
     rng = random.Random(131)
     sizes = [0, 1, 511, 512, 513, 1025, 0, 1, 7000, 3, 20000, 12, 4096, 1]
     keys = rand_keys(rng, sum(sizes), 0, 120)
@@ -528,12 +410,9 @@ def test_probe_multi_many_filters(dev, ab, oracle, F):
     assert np.array_equal(got, oracle.probe_multi(q, fid, flat, boff))
 
 
-@pytest.mark.parametrize("groups", [None, "2,4", "8,8", "1,3"])
 @pytest.mark.parametrize("bpk", [1, 3, 10, 40])
-def test_probe_read_grouping_all_k(dev, ab, oracle, bpk, groups, monkeypatch):
-    """k = 1, 2, 6, 27 under several read groupings (ADL_BLOOM_PROBE_GROUPS)."""
-    if groups:
-        monkeypatch.setenv("ADL_BLOOM_PROBE_GROUPS", groups)
+def test_probe_all_k(dev, ab, oracle, bpk):
+    """k = 1, 2, 6, 27 through the single-filter and the multi-filter probe."""
     keys = oracle.splitmix_keys16(0xABC, 20000)
     bm = oracle.keys2block(keys, bits_per_key=bpk)
     q = np.concatenate([keys[:5000], oracle.splitmix_keys16(0xABD, 30000)])
@@ -817,18 +696,23 @@ def test_build_maximum_filter(dev, ab, oracle):
 
 # ------------------------------------------------ SSTable build path (§8f rank 1)
 @pytest.mark.parametrize("mode", ["add", "batch"])
-@pytest.mark.parametrize("which", [1, 2])
+@pytest.mark.parametrize("which", [1, 2, 3])
 def test_sstable_writer_file_parity(dev, golden, oracle, tmp_path, mode, which):
     """test/sstable_test.cpp memtables flushed through the C++ SSTableWriter,
     filter built on the GPU: the file is byte-identical to the oracle's
-    restatement, and for BuildSSTable (:9-27) its name is the reference's oid."""
+    restatement, and for BuildSSTable (:9-27) its name is the reference's oid.
+    Memtables 2 (two versions per user key) and 3 (one to five) hold enough
+    adjacent duplicate user keys that Final skips them on the device
+    (ADL_BLOOM_SKIP_ADJACENT_DUPLICATES): the file must not change."""
     import sstable_oracle as S
 
     exe = os.path.join(ROOT, "adlsm-tree_amd", "bin", "sstable_test")
     args = [exe] + (["batch"] if mode == "batch" else []) + [str(which), str(tmp_path)]
     r = subprocess.run(args, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
-    oid, size = r.stdout.split()
+    oid, size, dups = r.stdout.split()
+    want_dups = {1: 0, 2: 5000, 3: sum((j * 7) % 5 for j in range(4000))}[which]
+    assert int(dups) == want_dups
     files = list(tmp_path.glob("*.sst"))
     assert [f.name for f in files] == [oid + ".sst"]
     got = files[0].read_bytes()

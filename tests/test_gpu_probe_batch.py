@@ -148,28 +148,6 @@ def test_probe_batch_sparse_runs(dev, ab, oracle, bpk):
     _check(dev, ab, oracle, arena, off, keys, fid, bpk=bpk)
 
 
-@pytest.mark.parametrize("split", [1, 2])
-def test_probe_batch_two_rounds(dev, ab, oracle, split, monkeypatch):
-    """The two-round binned probe (ADL_PB_SPLIT: bits 0 .. split-1 of every
-    query, then the other 6 - split bits of the queries still answered 1; the
-    batched form of the reference's early exit, src/filter_block.cpp:54-59).
-    Measured slower than one round, so not the default."""
-    monkeypatch.setenv("ADL_PB_SPLIT", str(split))
-    sizes = [1, 13, 50_000, 0, 300_000, 1_500_000, 7]
-    arena, off = _arena(oracle, sizes, seed0=1234)
-    rng = np.random.default_rng(split)
-    n = (1 << 20) + 4321
-    F = len(sizes)
-    fid = rng.integers(0, F + 1, n).astype(np.uint32)
-    keys = oracle.splitmix_keys16(17, n)
-    ins = rng.integers(0, 2, n).astype(bool)
-    for t, sz in enumerate(sizes):
-        sel = np.nonzero(ins & (fid == t))[0]
-        if sz and sel.size:
-            keys[sel] = oracle.splitmix_keys16(1234 + t, sz)[rng.integers(0, sz, sel.size)]
-    _check(dev, ab, oracle, arena, off, keys, fid)
-
-
 def test_probe_batch_many_chunks_one_filter(dev, ab, oracle):
     """One filter with more than 64 chunks per pb_tile wave (5.4 M queries:
     about 1 300 chunks of 4 096, 16 waves), so every wave stages its runs in

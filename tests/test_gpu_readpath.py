@@ -235,7 +235,7 @@ def test_pipeline_fixed_stride_unaligned_groups(dev, ab, oracle, stride):
 
 
 @pytest.mark.parametrize("pinned", [False, True])
-def test_pipeline_fault_mid_pipeline(dev, ab, oracle, monkeypatch, pinned):
+def test_pipeline_fault_mid_pipeline(dev, ab, oracle, knobs, pinned):
     """A build failing in group 2 (adl_bloom_test_fault) returns the error only
     after every copy into the caller's buffer has finished: the buffer does not
     change after the call returns.  The next call succeeds."""
@@ -252,7 +252,7 @@ def test_pipeline_fault_mid_pipeline(dev, ab, oracle, monkeypatch, pinned):
     else:
         keys, out = hk, np.zeros(total, dtype=np.uint8)
         view = lambda: out.copy()  # noqa: E731
-    monkeypatch.setenv("ADL_BLOOM_PIPE_MB", "32")  # groups of 5 filters: group 2 exists
+    knobs.set("ADL_BLOOM_PIPE_MB", "32")  # groups of 5 filters: group 2 exists
     ab.test_fault(ab.TEST_FAULT_PIPELINE_GROUP, 2)
     try:
         with pytest.raises(ab.AdlBloomError):
@@ -286,7 +286,7 @@ def _pack(keys):
 
 
 @pytest.mark.parametrize("bpk", [3, 10, 44])
-def test_probe_server_single_keys_vs_oracle(dev, ab, oracle, monkeypatch, bpk):
+def test_probe_server_single_keys_vs_oracle(dev, ab, oracle, knobs, bpk):
     """Batches of 1..8 queries (keys of 0..288 bytes, several tables, an
     uncached table, a filter index the block does not have) through the
     resident server equal the oracle and the launched probe."""
@@ -315,9 +315,9 @@ def test_probe_server_single_keys_vs_oracle(dev, ab, oracle, monkeypatch, bpk):
         got, unc = cache.probe(oids, table, data, offs)
         assert np.array_equal(got, want), (it, got, want)
         assert unc == int((table == T).sum())
-        monkeypatch.setenv("ADL_BLOOM_PROBE_SERVER", "0")
+        knobs.set("ADL_BLOOM_PROBE_SERVER", "0")
         got2, _ = cache.probe(oids, table, data, offs)
-        monkeypatch.delenv("ADL_BLOOM_PROBE_SERVER")
+        knobs.unset("ADL_BLOOM_PROBE_SERVER")
         assert np.array_equal(got2, want)
         # filter 1 does not exist in these one-filter blocks: absent
         got3, _ = cache.probe(oids, table, data, offs, filter=1)
@@ -327,12 +327,12 @@ def test_probe_server_single_keys_vs_oracle(dev, ab, oracle, monkeypatch, bpk):
     cache.close()
 
 
-def test_probe_server_relaunch_and_teardown(dev, ab, oracle, monkeypatch):
+def test_probe_server_relaunch_and_teardown(dev, ab, oracle, knobs):
     """A server that exits when idle (100 us) or at its life limit (2 ms) is
     relaunched by the next request; closing the cache while the server is
     running stops it; an armed completion fault fails one call only."""
-    monkeypatch.setenv("ADL_BLOOM_SERVER_IDLE_US", "100")
-    monkeypatch.setenv("ADL_BLOOM_SERVER_LIFE_US", "2000")
+    knobs.set("ADL_BLOOM_SERVER_IDLE_US", "100")
+    knobs.set("ADL_BLOOM_SERVER_LIFE_US", "2000")
     keys, blk = _block(oracle, 3100, 20_000)
     bm = oracle.keys2block(keys)
     q = np.concatenate([keys[:300], oracle.splitmix_keys16(0xD00D, 300)])
@@ -401,3 +401,49 @@ def test_probe_server_threads(dev, ab, oracle):
     cache.close()
     assert not errors, errors[:5]
     assert sorted(big_ms)[len(big_ms) // 2] < 15.0, big_ms
+
+
+def _readpath_json(args, timeout=300, **env):
+    import json
+
+    exe = os.path.join(ROOT, "adlsm-tree_amd", "bin", "readpath_test")
+    r = subprocess.run([exe] + args, capture_output=True, text=True, timeout=timeout, env=dict(os.environ, **env))
+    assert r.returncode == 0, r.stdout + r.stderr
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+def test_gets_beside_builds(dev, golden):
+    """Single-key Gets through the resident probe server while the headline
+    build and a configs[3]-shaped build (256 tables x 1 M keys) run on another
+    thread (the reference's DB::Get during DoCompaction, src/db.cpp:164-172,
+    263): every answer equals the one given with the GPU idle, the headline
+    bitmap equals the reference's SHA-256 and the 256 tables equal the oracle
+    pins, idle and concurrent alike.  The server's wave fits beside pass A
+    (2 KiB of LDS and 32 VGPRs left free on every CU), so the Gets do not
+    wait for a build; the times are printed (profiles/ holds the measured
+    runs)."""
+    import hashlib
+    import json
+
+    d = _readpath_json(["--coexist", "2"])
+    print(d)
+    assert d["get_mismatches"] == 0
+    sha10m = golden["appendix_b"]["bitmaps"][5]
+    assert sha10m["n"] == 10_000_000
+    assert d["headline_sha256"] == [sha10m["sha256"]] * 2
+    with open(os.path.join(ROOT, "tests", "golden", "full_size.json")) as f:
+        pins = json.load(f)["compaction"]
+    want = hashlib.sha256("".join(pins["bitmap_sha256"]).encode()).hexdigest()
+    assert d["compaction_sha_of_shas"] == [want, want]
+    assert d["get_us_during_builds"]["calls"] > 100
+
+
+def test_probe_server_tails(dev):
+    """20 000 single-key Gets in a row with a 2 ms server life: the requests
+    that meet an exiting server are answered by its last poll or by a
+    relaunch (no timeout path), every answer exact."""
+    d = _readpath_json(["--tails", "20000"], ADL_BLOOM_SERVER_LIFE_US="2000")
+    print(d)
+    assert d["mismatches"] == 0
+    assert d["single_key_us"]["calls"] == 20000
+    assert d["server_launches"] >= 10

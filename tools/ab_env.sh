@@ -1,6 +1,6 @@
 #!/bin/bash
 # tools/ab_env.sh -- interleaved A/B of bench.py under different env settings.
-# usage: AB="ADL_BLOOM_XCD_REMAP=0|ADL_BLOOM_XCD_REMAP=1" REPS=3 bash tools/ab_env.sh
+# usage: AB="ADL_BLOOM_CLAIM=0|ADL_BLOOM_CLAIM=1" REPS=3 bash tools/ab_env.sh
 set -u
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
