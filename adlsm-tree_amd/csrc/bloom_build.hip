@@ -915,6 +915,17 @@ __global__ __launch_bounds__(BLOCK) kPassARegs void bloom_bin16_kernel(BuildArgs
 #pragma unroll
           for (int j = 0; j < K; ++j) pos[i][j] = (h1[i] + (uint32_t)j * h2[i]) >> 3;
 #endif
+#ifdef ADL_BLOOM_STAMPS
+        // diagnostics: conflict-free LDS sort (wrong tiles, needs T >= 128 and
+        // no hash dedup).  Lane l counts into counter l, except that key slot 0
+        // of wave 0 puts its first position into counter 64 + l: a full chunk
+        // gives counters 0-63 an odd count each (16 waves x 6 keys x 6 - 1), so
+        // the scatter's 32 lanes of a group write 32 different banks too.
+        if (a.exp & 64)
+#pragma unroll
+          for (int j = 0; j < K; ++j)
+            pos[i][j] = (((uint32_t)(tid & 63) + (i == 0 && j == 0 && tid < 64 ? 64u : 0u)) << TL) | (pos[i][j] & tmask);
+#endif
         if constexpr (!CL)
 #pragma unroll
           for (int j = 0; j < K; ++j) atomicAdd(&hist[pos[i][j] >> TL], 1u);

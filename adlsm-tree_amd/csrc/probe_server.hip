@@ -39,8 +39,8 @@
 // build's persistent pass-A workgroup, which leaves exactly that free, so a
 // Get is served while a compaction builds (reference: DB::Get probes filters
 // without a lock while DoCompaction runs, src/db.cpp:164-172, 263, 294).  The
-// server runs on a stream of its own, created with a CU mask (all CUs), so no
-// other stream's work queues behind it on a shared hardware queue.
+// server runs on a stream of its own at the highest priority, so no other
+// stream's work queues behind it on a shared hardware queue (Server::create).
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>

@@ -43,6 +43,8 @@
 #include <thread>
 #include <vector>
 
+#include <sys/resource.h>
+
 #include <hip/hip_runtime_api.h>
 
 #include "adl_bloom.h"
@@ -202,9 +204,20 @@ void PrintLat(const char *name, const std::vector<double> &lat) {
          lat.empty() ? 0.0 : *std::max_element(lat.begin(), lat.end()));
 }
 
+// Context switches of the calling thread so far (voluntary + involuntary).
+long CtxSwitches() {
+  struct rusage ru;
+  if (getrusage(RUSAGE_THREAD, &ru)) return 0;
+  return ru.ru_nvcsw + ru.ru_nivcsw;
+}
+
 // Single-key IsKeyExists through the resident probe server, `calls` times in a
 // row: the latency distribution across the server's idle / life-limit exits
-// and relaunches (each relaunch is counted).
+// and relaunches (each relaunch is counted).  Each call is also tagged with
+// whether the thread was switched out during it (getrusage around the timed
+// window), and a host-only control runs the same number of ~5 us spins, so a
+// tail that comes from the operating system is told apart from one that comes
+// from the server.
 int Tails(size_t calls) {
   RC rc;
   Level lv = BuildLevel(4, 50000, 200000, &rc);
@@ -218,19 +231,22 @@ int Tails(size_t calls) {
   for (size_t i = 0; i < q.size(); ++i) want[i] = reader.IsKeyExists(0, q[i]);
   uint64_t l0 = 0, l1 = 0;
   if (adl_bloom_probe_server_launches(&l0)) return 1;
-  std::vector<double> lat, lat_relaunch, lat_plain;
+  std::vector<double> lat, lat_relaunch, lat_plain, lat_switched;
   lat.reserve(calls);
   size_t bad = 0;
   const double t_start = Now();
   uint64_t la = l0, lb = l0;
   for (size_t i = 0; i < calls; ++i) {
     const size_t j = i % q.size();
+    const long cs0 = CtxSwitches();
     const double t0 = Now();
     const bool hit = reader.IsKeyExists(0, q[j]);
     const double us = (Now() - t0) * 1e6;
+    const bool switched = CtxSwitches() != cs0;
     lat.push_back(us);
     (void)adl_bloom_probe_server_launches(&lb);
-    (lb != la ? lat_relaunch : lat_plain).push_back(us);
+    if (switched) lat_switched.push_back(us);
+    else (lb != la ? lat_relaunch : lat_plain).push_back(us);
     la = lb;
     bad += hit != (want[j] != 0);
     if (i % 2000 == 1999)
@@ -239,18 +255,36 @@ int Tails(size_t calls) {
   }
   const double elapsed = Now() - t_start;
   if (adl_bloom_probe_server_launches(&l1)) return 1;
+  // host-only control: spins of the median call's length, timed the same way
+  const double spin_us = Pct(lat, 0.5);
+  std::vector<double> ctl;
+  ctl.reserve(calls);
+  for (size_t i = 0; i < calls; ++i) {
+    const double t0 = Now();
+    while ((Now() - t0) * 1e6 < spin_us) {
+    }
+    ctl.push_back((Now() - t0) * 1e6);
+  }
   std::vector<double> top = lat;
   std::sort(top.rbegin(), top.rend());
   top.resize(std::min<size_t>(top.size(), 12));
-  size_t over30 = 0;
-  for (double v : lat) over30 += v > 30.0;
+  auto over = [](const std::vector<double> &v, double x) {
+    size_t c = 0;
+    for (double u : v) c += u > x;
+    return c;
+  };
   printf("{");
   PrintLat("single_key_us", lat);
   printf(", ");
   PrintLat("calls_that_relaunched_us", lat_relaunch);
   printf(", ");
   PrintLat("other_calls_us", lat_plain);
-  printf(", \"over_30us\": %zu, \"top_us\": [", over30);
+  printf(", ");
+  PrintLat("calls_switched_out_us", lat_switched);
+  printf(", ");
+  PrintLat("host_spin_control_us", ctl);
+  printf(", \"over_30us\": %zu, \"over_30us_not_switched_out\": %zu, \"control_over_30us\": %zu, \"top_us\": [",
+         over(lat, 30.0), over(lat_plain, 30.0) + over(lat_relaunch, 30.0), over(ctl, 30.0));
   for (size_t i = 0; i < top.size(); ++i) printf("%s%.1f", i ? ", " : "", top[i]);
   printf("], \"elapsed_s\": %.3f, \"server_launches\": %llu, \"mismatches\": %zu}\n", elapsed,
          (unsigned long long)(l1 - l0), bad);
@@ -266,7 +300,8 @@ int Tails(size_t calls) {
 // server while another runs the headline build (10 M 16-byte keys, one
 // filter) and a configs[3]-shaped segmented build (256 tables x 1 M keys)
 // back to back on its own stream.  Phases: builds alone, Gets alone, both.
-// Prints one JSON line: build times and Get latencies idle and concurrent,
+// Prints one JSON line: build times and Get latencies idle and concurrent
+// (calls during which the OS switched the thread out are counted apart),
 // the headline bitmap's SHA-256 and the SHA-256 of the 256 tables' SHA-256
 // hex digests (idle and concurrent), and the Get mismatches.
 struct DevBuf {
@@ -356,15 +391,18 @@ int Coexist(int reps) {
   if (!shas(sha1_idle, shac_idle)) return 1;
   // phase 2: Gets alone
   std::vector<double> get_idle, get_conc;
-  size_t bad = 0;
-  auto one_get = [&](size_t i, std::vector<double> &lat) {
+  size_t bad = 0, switched_idle = 0, switched_conc = 0;
+  auto one_get = [&](size_t i, std::vector<double> &lat, size_t &switched) {
     const size_t j = i % q.size();
+    const long cs0 = CtxSwitches();
     const double t0 = Now();
     const bool hit = reader.IsKeyExists(0, q[j]);
-    lat.push_back((Now() - t0) * 1e6);
+    const double us = (Now() - t0) * 1e6;
+    if (CtxSwitches() != cs0) ++switched;  // the OS took the thread: not the server's latency
+    else lat.push_back(us);
     bad += hit != (want[j] != 0);
   };
-  for (size_t i = 0; i < 50000; ++i) one_get(i, get_idle);
+  for (size_t i = 0; i < 50000; ++i) one_get(i, get_idle, switched_idle);
   // phase 3: both
   std::atomic<bool> building{true};
   std::atomic<int> build_fail{0};
@@ -377,7 +415,7 @@ int Coexist(int reps) {
     }
     building = false;
   });
-  for (size_t i = 0; building.load(); ++i) one_get(i, get_conc);
+  for (size_t i = 0; building.load(); ++i) one_get(i, get_conc, switched_conc);
   builder.join();
   if (build_fail || !shas(sha1_conc, shac_conc)) return 1;
   uint64_t launches = 0;
@@ -392,6 +430,7 @@ int Coexist(int reps) {
   PrintLat("get_us_idle", get_idle);
   printf(", ");
   PrintLat("get_us_during_builds", get_conc);
+  printf(", \"gets_switched_out\": [%zu, %zu]", switched_idle, switched_conc);
   printf(", \"get_mismatches\": %zu, \"headline_sha256\": [\"%s\", \"%s\"], \"compaction_sha_of_shas\": [\"%s\", \"%s\"], "
          "\"server_launches\": %llu}\n",
          bad, sha1_idle.c_str(), sha1_conc.c_str(), shac_idle.c_str(), shac_conc.c_str(),
