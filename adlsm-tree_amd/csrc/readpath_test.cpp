@@ -301,7 +301,8 @@ int Tails(size_t calls) {
 // filter) and a configs[3]-shaped segmented build (256 tables x 1 M keys)
 // back to back on its own stream.  Phases: builds alone, Gets alone, both.
 // Prints one JSON line: build times and Get latencies idle and concurrent
-// (calls during which the OS switched the thread out are counted apart),
+// (calls during which the OS switched the thread out are counted apart, and
+// calls that had to launch the server are reported apart),
 // the headline bitmap's SHA-256 and the SHA-256 of the 256 tables' SHA-256
 // hex digests (idle and concurrent), and the Get mismatches.
 struct DevBuf {
@@ -391,18 +392,22 @@ int Coexist(int reps) {
   if (!shas(sha1_idle, shac_idle)) return 1;
   // phase 2: Gets alone
   std::vector<double> get_idle, get_conc;
+  std::vector<double> relaunch_idle, relaunch_conc;  // calls that (re)launched the server
   size_t bad = 0, switched_idle = 0, switched_conc = 0;
-  auto one_get = [&](size_t i, std::vector<double> &lat, size_t &switched) {
+  auto one_get = [&](size_t i, std::vector<double> &lat, std::vector<double> &relaunched, size_t &switched) {
     const size_t j = i % q.size();
+    uint64_t la = 0, lb = 0;
+    (void)adl_bloom_probe_server_launches(&la);
     const long cs0 = CtxSwitches();
     const double t0 = Now();
     const bool hit = reader.IsKeyExists(0, q[j]);
     const double us = (Now() - t0) * 1e6;
+    (void)adl_bloom_probe_server_launches(&lb);
     if (CtxSwitches() != cs0) ++switched;  // the OS took the thread: not the server's latency
-    else lat.push_back(us);
+    else (lb != la ? relaunched : lat).push_back(us);
     bad += hit != (want[j] != 0);
   };
-  for (size_t i = 0; i < 50000; ++i) one_get(i, get_idle, switched_idle);
+  for (size_t i = 0; i < 50000; ++i) one_get(i, get_idle, relaunch_idle, switched_idle);
   // phase 3: both
   std::atomic<bool> building{true};
   std::atomic<int> build_fail{0};
@@ -415,7 +420,7 @@ int Coexist(int reps) {
     }
     building = false;
   });
-  for (size_t i = 0; building.load(); ++i) one_get(i, get_conc, switched_conc);
+  for (size_t i = 0; building.load(); ++i) one_get(i, get_conc, relaunch_conc, switched_conc);
   builder.join();
   if (build_fail || !shas(sha1_conc, shac_conc)) return 1;
   uint64_t launches = 0;
@@ -430,6 +435,10 @@ int Coexist(int reps) {
   PrintLat("get_us_idle", get_idle);
   printf(", ");
   PrintLat("get_us_during_builds", get_conc);
+  printf(", ");
+  PrintLat("relaunching_gets_us_idle", relaunch_idle);
+  printf(", ");
+  PrintLat("relaunching_gets_us_during_builds", relaunch_conc);
   printf(", \"gets_switched_out\": [%zu, %zu]", switched_idle, switched_conc);
   printf(", \"get_mismatches\": %zu, \"headline_sha256\": [\"%s\", \"%s\"], \"compaction_sha_of_shas\": [\"%s\", \"%s\"], "
          "\"server_launches\": %llu}\n",
