@@ -364,16 +364,20 @@ def probe_multi(keys, filter_id, bitmaps, bitmap_off, offsets=None, bits_per_key
 
 
 def probe_batch(keys, filter_id, bitmaps, bitmap_off, offsets=None, bits_per_key: int = 10, stream=None,
-                bitmap_end=None):
+                bitmap_end=None, out=None):
     """Large-batch multi-filter probe (adl_bloom_probe_batch_device): the answers of
     probe_multi, through the tile-binned pipeline when the batch is large.  The
-    workspace comes from torch's caching allocator."""
+    workspace comes from torch's caching allocator.  `out`: an optional uint8
+    device tensor of at least n bytes (any alignment) to answer into."""
     pk, po, n, stride = _keyset(keys, offsets)
     F = bitmap_off.numel() - (0 if bitmap_end is not None else 1)
     L = lib()
     wsb = L.adl_bloom_probe_batch_workspace_bytes(n, F, bits_per_key, stride)
     ws = empty_device(wsb, keys.device)
-    out = _torch().empty(max(n, 1), dtype=_torch().uint8, device=keys.device)
+    if out is None:
+        out = _torch().empty(max(n, 1), dtype=_torch().uint8, device=keys.device)
+    elif out.dtype != _torch().uint8 or out.numel() < n or not out.is_contiguous():
+        raise ValueError("out must be a contiguous uint8 tensor of at least n elements")
     _check(L.adl_bloom_probe_batch_device(pk, po, n, stride, _dptr(filter_id), F, _dptr(bitmaps), _dptr(bitmap_off),
                                           _dptr(bitmap_end), bits_per_key, _dptr(out), _dptr(ws), wsb,
                                           _stream(stream)), "adl_bloom_probe_batch_device")

@@ -283,11 +283,12 @@ __global__ __launch_bounds__(kBlk) void pb_starts_kernel(const uint32_t *__restr
 // A block's runs: filter f's queries of block b go to slots [lstart[f],
 // lstart[f] + lcnt[f]) in filter order and to places [lbase[f], ...) of the
 // block's own sorted order.  Loads lcnt, lstart (and ltiles) and scans lbase.
+template <int BLK = kBlk>
 __device__ __forceinline__ void load_runs(const uint32_t *cnt, const uint32_t *start, uint32_t nb, uint32_t F,
                                           const PFilter *desc, uint32_t *lcnt, uint32_t *lstart, uint32_t *lbase,
                                           uint32_t *ltiles, uint32_t *scratch) {
   const uint64_t row = (uint64_t)blockIdx.x * (F + 1);  // block-major
-  for (uint32_t f = threadIdx.x; f <= F; f += kBlk) {
+  for (uint32_t f = threadIdx.x; f <= F; f += BLK) {
     const uint32_t c = cnt[row + f];
     lcnt[f] = c;
     lbase[f] = c;
@@ -295,7 +296,7 @@ __device__ __forceinline__ void load_runs(const uint32_t *cnt, const uint32_t *s
     if (ltiles && f < F) ltiles[f] = desc[f].tiles;
   }
   __syncthreads();
-  block_excl_scan_array<kBlk>(lbase, F + 1, scratch);
+  block_excl_scan_array<BLK>(lbase, F + 1, scratch);
 }
 
 // ---------------------------------------------------------------- K3
@@ -683,59 +684,79 @@ __global__ __launch_bounds__(kBlk) void pb_tile_kernel(const uint8_t *__restrict
 }
 
 // ---------------------------------------------------------------- K6
-__global__ __launch_bounds__(kBlk) void pb_gather_kernel(const uint16_t *__restrict__ dest,
-                                                         const uint8_t *__restrict__ res, uint64_t n, uint32_t F,
-                                                         uint32_t nb, const uint32_t *__restrict__ cnt,
-                                                         const uint32_t *__restrict__ start,
-                                                         uint8_t *__restrict__ out) {
+// Per block: the answers of its runs, gathered run by run into an LDS bit
+// array in the block's sorted order, then out[i] = the bit at the query's
+// place (coalesced).  Thread f takes filter f's run: its cleared bits are a
+// contiguous range of the answer array (filter order), read 32 at a time as
+// a funnel of two words and ORed into the LDS bits at the run's place: about
+// two loads per run instead of one per query, and no per-query search.
+// Small workgroups (kGatherBlk threads), so several blocks per CU overlap
+// their round trips.
+constexpr int kGatherBlk = 256;
+__global__ __launch_bounds__(kGatherBlk) void pb_gather_kernel(const uint16_t *__restrict__ dest,
+                                                               const uint8_t *__restrict__ res, uint64_t n, uint32_t F,
+                                                               uint32_t nb, const uint32_t *__restrict__ cnt,
+                                                               const uint32_t *__restrict__ start,
+                                                               uint8_t *__restrict__ out) {
+  constexpr int B = kGatherBlk;
+  constexpr uint32_t QPT = kQB / B;  // queries per thread
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-  uint8_t *lres = reinterpret_cast<uint8_t *>(lds);  // kQB answers in the block's filter order
-  uint32_t *lcnt = lds + kQB / 4, *lstart = lcnt + F + 1, *lbase = lstart + F + 1, *scratch = lbase + F + 1;
+  uint32_t *lbits = lds;  // kQB cleared bits in the block's sorted order
+  uint32_t *lcnt = lds + kQB / 32, *lstart = lcnt + F + 1, *lbase = lstart + F + 1, *scratch = lbase + F + 1;
   const int tid = threadIdx.x;
-  // this thread's queries' places: in flight while the block's runs are set up
-  const uint64_t i0 = (uint64_t)blockIdx.x * kQB + tid;
-  uint16_t pl_q[kQPT];
+  const uint32_t *clrw = reinterpret_cast<const uint32_t *>(res);
+  // this thread's queries' places (coalesced 16-byte loads: 8 places each),
+  // in flight while the block's runs are set up
+  const uint64_t i0 = (uint64_t)blockIdx.x * kQB;
+  const uint32_t nq = (uint32_t)min((uint64_t)kQB, n - i0);
+  uint4 pv[QPT / 8];
 #pragma unroll
-  for (uint32_t r = 0; r < kQPT; ++r) {
-    const uint64_t i = i0 + (uint64_t)r * kBlk;
-    pl_q[r] = i < n ? dest[i] : kNoSlot;
-  }
-  load_runs(cnt, start, nb, F, nullptr, lcnt, lstart, lbase, nullptr, scratch);
-  // place p of the block's sorted order belongs to the filter whose run holds
-  // it (the last f with lbase[f] <= p, runs of the same filter are
-  // contiguous); all kQPT loads of a thread are in flight together
-  const uint32_t nvalid = lbase[F];
-  // every gather is issued unconditionally (a place past the block's last
-  // valid one reads that one and is masked), so all kQPT are in flight at once
-  uint8_t v[kQPT];
-  uint32_t src[kQPT];
-#pragma unroll
-  for (uint32_t r = 0; r < kQPT; ++r) {
-    const uint32_t pl = min(tid + r * kBlk, nvalid ? nvalid - 1u : 0u);
-    uint32_t lo = 0, hi = F;  // lbase[lo] <= pl < lbase[hi]
-    while (hi - lo > 1) {
-      const uint32_t mid = (lo + hi) >> 1;
-      if (lbase[mid] <= pl) lo = mid; else hi = mid;
+  for (uint32_t r = 0; r < QPT / 8; ++r) {
+    const uint32_t q = (tid + r * B) * 8;  // the block's first query of these 8
+    pv[r] = q + 8 <= nq ? *reinterpret_cast<const uint4 *>(dest + i0 + q) : make_uint4(~0u, ~0u, ~0u, ~0u);
+    if (q < nq && q + 8 > nq) {  // the block's ragged end
+      uint16_t t[8];
+      for (uint32_t u = 0; u < 8; ++u) t[u] = q + u < nq ? dest[i0 + q + u] : kNoSlot;
+      pv[r] = make_uint4(t[0] | (uint32_t)t[1] << 16, t[2] | (uint32_t)t[3] << 16, t[4] | (uint32_t)t[5] << 16,
+                         t[6] | (uint32_t)t[7] << 16);
     }
-    src[r] = lstart[lo] + (pl - lbase[lo]);
   }
-#pragma unroll
-  for (uint32_t r = 0; r < kQPT; ++r)
-    v[r] = nvalid ? (uint8_t)(((reinterpret_cast<const uint32_t *>(res)[src[r] >> 5] >> (src[r] & 31)) & 1u) ^ 1u)
-                  : (uint8_t)0;
-#pragma unroll
-  for (uint32_t r = 0; r < kQPT; ++r)
-    if (tid + r * kBlk >= nvalid) v[r] = 0;
-#pragma unroll
-  for (uint32_t r = 0; r < kQPT; ++r) {
-    const uint32_t pl = tid + r * kBlk;
-    if (pl < nvalid) lres[pl] = v[r];
+  for (uint32_t w = tid; w < kQB / 32; w += B) lbits[w] = 0u;
+  load_runs<B>(cnt, start, nb, F, nullptr, lcnt, lstart, lbase, nullptr, scratch);
+  for (uint32_t f = tid; f < F; f += B) {
+    const uint32_t c = lcnt[f];
+    const uint32_t s0 = lstart[f], p0 = lbase[f];
+    for (uint32_t o = 0; o < c; o += 32) {
+      const uint32_t s = s0 + o, p = p0 + o, len = min(32u, c - o);
+      const uint32_t sh = s & 31u;
+      const uint32_t w0 = clrw[s >> 5], w1 = clrw[(s >> 5) + 1];  // (the array has 64 bytes of slack)
+      uint32_t v = sh ? (w0 >> sh) | (w1 << (32u - sh)) : w0;
+      if (len < 32) v &= (1u << len) - 1u;
+      if (!v) continue;
+      const uint32_t ps = p & 31u;
+      atomicOr(&lbits[p >> 5], v << ps);
+      if (ps && ps + len > 32) atomicOr(&lbits[(p >> 5) + 1], v >> (32u - ps));
+    }
   }
   __syncthreads();
 #pragma unroll
-  for (uint32_t r = 0; r < kQPT; ++r) {
-    const uint64_t i = i0 + (uint64_t)r * kBlk;
-    if (i < n) out[i] = pl_q[r] == kNoSlot ? 0 : lres[pl_q[r]];
+  for (uint32_t r = 0; r < QPT / 8; ++r) {
+    const uint32_t q = (tid + r * B) * 8;
+    if (q >= nq) continue;
+    const uint32_t pw[4] = {pv[r].x, pv[r].y, pv[r].z, pv[r].w};
+    uint32_t lo = 0, hi = 0;
+#pragma unroll
+    for (uint32_t u = 0; u < 8; ++u) {
+      const uint32_t pl = (pw[u / 2] >> (16 * (u & 1))) & 0xFFFFu;
+      // answer 1 iff the query was probed (a place) and none of its bits was clear
+      const uint32_t a = pl == kNoSlot ? 0u : ((lbits[pl >> 5] >> (pl & 31u)) & 1u) ^ 1u;
+      if (u < 4) lo |= a << (8 * u); else hi |= a << (8 * (u - 4));
+    }
+    if (q + 8 <= nq && (reinterpret_cast<uintptr_t>(out) & 7u) == 0) {
+      *reinterpret_cast<uint2 *>(out + i0 + q) = make_uint2(lo, hi);
+    } else {
+      for (uint32_t u = 0; u < 8 && q + u < nq; ++u) out[i0 + q + u] = (uint8_t)(((u < 4 ? lo : hi) >> (8 * (u & 3))) & 1u);
+    }
   }
 }
 
@@ -789,7 +810,7 @@ int adl_bloom_probe_batch_device(const uint8_t *d_keys, const uint64_t *d_offset
   const uint32_t cus = adl_host::device_cus();
   const size_t lds_k1 = (size_t)(2 * F + 2) * 4;                       // counters + tile counts
   const size_t lds_k3 = (size_t)(2 * kQB + 5 * (F + 1) + 32) * 4;      // hashes + 5 per-filter arrays + scratch
-  const size_t lds_k6 = (size_t)(kQB / 4 + 3 * (F + 1) + 32) * 4;      // answers + 3 per-filter arrays + scratch
+  const size_t lds_k6 = (size_t)(kQB / 32 + 3 * (F + 1) + 32) * 4;     // answer bits + 3 per-filter arrays + scratch
   const size_t lds_p1 = (size_t)(kMaxTiles + 4 + 64 + p.k * p.C) * 4;
   const size_t lds_p2 = (size_t)kTileBytes + 64 + (size_t)((F + 1 + 3) & ~3u) * 4 +
                         (size_t)(kBlk / kWave) * kMaskWords * 4;
@@ -828,7 +849,7 @@ int adl_bloom_probe_batch_device(const uint8_t *d_keys, const uint64_t *d_offset
                                 : bin(adl_host::lds_limit<pb_bin_kernel<0>>, pb_bin_kernel<0>);
     if (rc_bin != ADL_OK) return rc_bin;
     if (int rc = adl_host::lds_limit<pb_gather_kernel>()) return rc;
-    hipLaunchKernelGGL(pb_gather_kernel, dim3(p.nb), dim3(kBlk), lds_k6, st, dest, res, n, F, p.nb, cnt, start,
+    hipLaunchKernelGGL(pb_gather_kernel, dim3(p.nb), dim3(kGatherBlk), lds_k6, st, dest, res, n, F, p.nb, cnt, start,
                        d_out);
     ADL_HIP_TRY(hipGetLastError());
     return ADL_OK;

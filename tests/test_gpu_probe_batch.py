@@ -92,6 +92,23 @@ def test_probe_batch_threshold(dev, ab, oracle, n):
     _check(dev, ab, oracle, arena, off, k, f)
 
 
+@pytest.mark.parametrize("shift", [1, 3, 8])
+def test_probe_batch_unaligned_out(dev, ab, oracle, shift):
+    """Answers written through an output pointer at any byte offset, and a batch
+    whose last bucketing block is ragged (n not a multiple of 8 or 8192)."""
+    T, n = 8, (1 << 20) + 8195
+    arena, off = _arena(oracle, [30_000] * T)
+    k, f, _ = oracle.synth_probe_queries(n, num_tables=T, keys_per_table=30_000)
+    want = oracle.probe_multi(k, f, arena, off)
+    buf = dev.full((n + 16,), 0xAB, dtype=dev.uint8, device="cuda")
+    view = buf[shift:shift + n]
+    ab.probe_batch(dev.from_numpy(k).cuda(), dev.from_numpy(f.view(np.int32)).cuda(), dev.from_numpy(arena).cuda(),
+                   dev.from_numpy(off.view(np.int64)).cuda(), out=view)
+    got = buf.cpu().numpy()
+    assert np.array_equal(got[shift:shift + n], want)
+    assert (got[:shift] == 0xAB).all() and (got[shift + n:] == 0xAB).all()  # nothing written outside
+
+
 def test_probe_batch_ranges_with_gaps(dev, ab, oracle):
     """Filters anywhere in an arena (begin/end per filter, gaps and any order),
     as the filter cache lays them out."""
