@@ -474,7 +474,8 @@ __global__ __launch_bounds__(kBlk) void pb_bin_kernel(const uint2 *__restrict__ 
 // registers at the tile's start and keeps two runs' loads in flight.
 constexpr uint32_t kTileVecPT = kTileBytes / 16 / kBlk;  // 16-byte tile vectors per thread
 constexpr int kRunLoads = 6;                             // entries per run per stage: 6 x 64 (runs average ~320)
-constexpr uint32_t kMaskWords = (kMaxC + 31) / 32 + 1;   // a wave's cleared-bit mask of one chunk (+ its shift)
+constexpr uint32_t kMaskW64 = (kMaxC + 63) / 64 + 1;     // a wave's cleared-bit mask of one chunk (+ its shift), u64 words
+constexpr uint32_t kMaskWords = 2 * kMaskW64;
 
 struct TileRef {
   uint32_t f, t, sh, nvec, tail;
@@ -516,24 +517,26 @@ __global__ __launch_bounds__(kBlk) void pb_tile_kernel(const uint8_t *__restrict
   const int tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid / kWave;
   // A clear bit sets its query's "cleared" bit.  Each wave gathers the bits
   // of the run (one chunk) it is testing in a private LDS mask of the chunk's
-  // 4 096 slots (shifted by the chunk's first slot mod 32), and ORs the mask's
-  // nonzero words into the global bit array with coalesced device-scope
-  // atomics when it moves to its next run: about 129 word atomics per run
-  // instead of ~1 200 scattered byte stores.  The flush is issued after a
-  // stage's tests and before the next stage's loads, so only the wait for the
-  // stage already in flight can include it.
-  uint32_t *clrw = reinterpret_cast<uint32_t *>(res);
-  uint32_t *zmaskw = lds + (kTileBytes + 64) / 4 + ((F + 1 + 3) & ~3u) + (uint32_t)wave * kMaskWords;
+  // 4 096 slots (shifted by the chunk's first slot mod 64), and ORs the mask's
+  // nonzero 64-bit words into the global bit array with coalesced
+  // device-scope atomics when it moves to its next run: one or two atomic
+  // wave-instructions per run (65 words) instead of ~1 200 scattered byte
+  // stores.  The flush is issued after a stage's tests and before the next
+  // stage's loads, so only the wait for the stage already in flight can
+  // include it.
+  unsigned long long *clr64 = reinterpret_cast<unsigned long long *>(res);  // (the workspace area is 256-B aligned)
+  uint32_t *zmaskw = lds + (kTileBytes + 64) / 4 + ((F + 1 + 3) & ~3u) + (uint32_t)wave * kMaskWords;  // 8-B aligned
+  unsigned long long *zmask64 = reinterpret_cast<unsigned long long *>(zmaskw);
   for (uint32_t w = (uint32_t)lane; w < kMaskWords; w += kWave) zmaskw[w] = 0u;
   auto flush_run = [&](uint32_t rq) {
 #pragma unroll
-    for (uint32_t k2 = 0; k2 < 3; ++k2) {
+    for (uint32_t k2 = 0; k2 < 2; ++k2) {
       const uint32_t w = (uint32_t)lane + k2 * kWave;
-      if (w < kMaskWords) {
-        const uint32_t v = zmaskw[w];
+      if (w < kMaskW64) {
+        const unsigned long long v = zmask64[w];
         if (v) {
-          atomicOr(&clrw[(rq >> 5) + w], v);
-          zmaskw[w] = 0u;
+          atomicOr(&clr64[(rq >> 6) + w], v);
+          zmask64[w] = 0ull;
         }
       }
     }
@@ -626,7 +629,7 @@ __global__ __launch_bounds__(kBlk) void pb_tile_kernel(const uint8_t *__restrict
     // issue back to back), then the clear bits go to the zero ring
     auto consume = [&](const Stage &sg, const Stage &nx) {
       const uint32_t rq = d.qbase + sg.jc * C;  // the chunk's first answer (n < 2^31)
-      const uint32_t rs = rq & 31u;
+      const uint32_t rs = rq & 63u;
       uint32_t w[kRunLoads];
 #pragma unroll
       for (int u = 0; u < kRunLoads; ++u) w[u] = ltile[((sg.x[u] & ((1u << kTL) - 1u)) + now.sh) >> 5];
