@@ -155,6 +155,17 @@ __device__ __forceinline__ uint32_t bucket_of(uint32_t f, uint32_t F, const uint
   return (f < F && ltiles[f]) ? f : F;
 }
 
+// The bucketing block a workgroup of a per-block kernel (K3, K6) takes:
+// consecutive blocks on one XCD (workgroup i runs on XCD i % 8), so the runs
+// of neighbouring blocks -- adjacent in filter order, sharing the cache line
+// where one ends and the next begins -- are written (K3) and read (K6)
+// through one L2, which merges the two partial-line writes.  A bijection on
+// [0, nb) for any nb.
+__device__ __forceinline__ uint32_t xcd_block(uint32_t nb) {
+  const uint32_t x = blockIdx.x % 8, i = blockIdx.x / 8, q = nb / 8, r = nb % 8;
+  return x * q + min(x, r) + i;
+}
+
 // ---------------------------------------------------------------- K1
 __global__ __launch_bounds__(kBlk) void pb_hist_kernel(const uint32_t *__restrict__ fid, uint64_t n, uint32_t F,
                                                        uint32_t nb, const PFilter *__restrict__ desc,
@@ -284,10 +295,10 @@ __global__ __launch_bounds__(kBlk) void pb_starts_kernel(const uint32_t *__restr
 // lstart[f] + lcnt[f]) in filter order and to places [lbase[f], ...) of the
 // block's own sorted order.  Loads lcnt, lstart (and ltiles) and scans lbase.
 template <int BLK = kBlk>
-__device__ __forceinline__ void load_runs(const uint32_t *cnt, const uint32_t *start, uint32_t nb, uint32_t F,
+__device__ __forceinline__ void load_runs(const uint32_t *cnt, const uint32_t *start, uint32_t b, uint32_t F,
                                           const PFilter *desc, uint32_t *lcnt, uint32_t *lstart, uint32_t *lbase,
                                           uint32_t *ltiles, uint32_t *scratch) {
-  const uint64_t row = (uint64_t)blockIdx.x * (F + 1);  // block-major
+  const uint64_t row = (uint64_t)b * (F + 1);  // block-major
   for (uint32_t f = threadIdx.x; f <= F; f += BLK) {
     const uint32_t c = cnt[row + f];
     lcnt[f] = c;
@@ -318,7 +329,8 @@ __global__ __launch_bounds__(kBlk) void pb_scatter_kernel(const uint4 *__restric
   // every query's id and key are requested first (unconditionally: a lane
   // past n loads the last query and discards it), so they land while the
   // block's runs are set up
-  const uint64_t i0 = (uint64_t)blockIdx.x * kQB + tid;
+  const uint32_t blk = xcd_block(nb);
+  const uint64_t i0 = (uint64_t)blk * kQB + tid;
   uint32_t fq[kQPT];
   uint4 kq[kQPT];
 #pragma unroll
@@ -327,7 +339,7 @@ __global__ __launch_bounds__(kBlk) void pb_scatter_kernel(const uint4 *__restric
     fq[r] = fid[i];
     kq[r] = load_nt(keys + i);
   }
-  load_runs(cnt, start, nb, F, desc, lcnt, lstart, lbase, ltiles, scratch);
+  load_runs(cnt, start, blk, F, desc, lcnt, lstart, lbase, ltiles, scratch);
   for (uint32_t f = tid; f <= F; f += kBlk) lcur[f] = lbase[f];
   __syncthreads();
 #pragma unroll
@@ -710,7 +722,8 @@ __global__ __launch_bounds__(kGatherBlk) void pb_gather_kernel(const uint16_t *_
   const uint32_t *clrw = reinterpret_cast<const uint32_t *>(res);
   // this thread's queries' places (coalesced 16-byte loads: 8 places each),
   // in flight while the block's runs are set up
-  const uint64_t i0 = (uint64_t)blockIdx.x * kQB;
+  const uint32_t blk = xcd_block(nb);
+  const uint64_t i0 = (uint64_t)blk * kQB;
   const uint32_t nq = (uint32_t)min((uint64_t)kQB, n - i0);
   uint4 pv[QPT / 8];
 #pragma unroll
@@ -725,7 +738,7 @@ __global__ __launch_bounds__(kGatherBlk) void pb_gather_kernel(const uint16_t *_
     }
   }
   for (uint32_t w = tid; w < kQB / 32; w += B) lbits[w] = 0u;
-  load_runs<B>(cnt, start, nb, F, nullptr, lcnt, lstart, lbase, nullptr, scratch);
+  load_runs<B>(cnt, start, blk, F, nullptr, lcnt, lstart, lbase, nullptr, scratch);
   for (uint32_t f = tid; f < F; f += B) {
     const uint32_t c = lcnt[f];
     const uint32_t s0 = lstart[f], p0 = lbase[f];
