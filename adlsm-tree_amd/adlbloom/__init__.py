@@ -433,8 +433,11 @@ def profile_collect():
 
 
 # ------------------------------------------------------------------ host-pointer API
-def build_host(keys: np.ndarray, offsets: np.ndarray | None = None, bits_per_key: int = 10) -> np.ndarray:
-    """adl_bloom_build: host keys in, host bitmap out (upload + build + download)."""
+def build_host(keys: np.ndarray, offsets: np.ndarray | None = None, bits_per_key: int = 10,
+               out: np.ndarray | None = None) -> np.ndarray:
+    """adl_bloom_build: host keys in, host bitmap out (upload + build + download).
+    `out`: an optional uint8 host array (any alignment; pinned or pageable) of
+    at least the bitmap's size to write it into."""
     keys = np.ascontiguousarray(keys, dtype=np.uint8)
     if offsets is None:
         n, stride, po = keys.shape[0], keys.shape[1], None
@@ -444,10 +447,13 @@ def build_host(keys: np.ndarray, offsets: np.ndarray | None = None, bits_per_key
     nb = bitmap_bytes(n, bits_per_key)
     if nb == 0:
         raise AdlBloomError(-2, "bitmap size")
-    out = np.empty(nb, dtype=np.uint8)
+    if out is None:
+        out = np.empty(nb, dtype=np.uint8)
+    elif out.dtype != np.uint8 or out.size < nb or not out.flags["C_CONTIGUOUS"]:
+        raise ValueError("out must be a contiguous uint8 array of at least the bitmap's size")
     kp = keys.ctypes.data if keys.size else np.zeros(1, np.uint8).ctypes.data
     _check(lib().adl_bloom_build(kp, po, n, stride, bits_per_key, out.ctypes.data, None), "adl_bloom_build")
-    return out
+    return out[:nb]
 
 
 def probe_host(keys: np.ndarray, bitmap: np.ndarray, offsets: np.ndarray | None = None,

@@ -1926,43 +1926,18 @@ int adl_bloom_build_segmented_device_ex(const uint8_t *d_keys, const uint64_t *d
   }
 }
 
+// One filter from host memory: the pipelined host build with one filter
+// (bloom_pipeline.hip), so pinned keys and a pinned bitmap are DMAed directly
+// and pageable ones go through one staging copy each way (this
+// entry point used to copy every key into staging, then the bitmap out of it).
 int adl_bloom_build(const uint8_t *h_keys, const uint64_t *h_offsets, uint64_t n,
                     uint32_t key_stride, int32_t bits_per_key, uint8_t *h_bitmap, void *stream) {
-  try {
-    if (!h_bitmap || (n && !h_keys)) return ADL_ERR_INVALID_ARG;
-    if (!h_offsets && n && key_stride == 0) return ADL_ERR_INVALID_ARG;
-    const uint64_t bytes = adl_host::bitmap_bytes(n, bits_per_key);
-    if (!bytes) return bits_per_key < 0 ? ADL_ERR_INVALID_ARG : ADL_ERR_TOO_LARGE;
-    hipStream_t st = adl_host::sync_stream(stream);
-    const uint64_t key_bytes = h_offsets ? (n ? h_offsets[n] : 0) : n * (uint64_t)key_stride;
-    const uint64_t alloc = adl_host::round_up(bytes, 16);
-    const uint64_t ws = adl_bloom_build_workspace_bytes(&n, 1, bits_per_key);
-    const uint64_t off_bytes = h_offsets ? (n + 1) * 8 : 0;
-    // device: [keys | offsets | bitmap | workspace]; pinned host: [keys | offsets], then the bitmap
-    const uint64_t o_offs = adl_host::round_up(key_bytes + 16, 256);
-    const uint64_t o_bm = o_offs + adl_host::round_up(off_bytes, 256);
-    const uint64_t o_ws = o_bm + adl_host::round_up(alloc, 256);
-    adl_host::Staging &sg = adl_host::t_stage;
-    int rc = sg.reserve(std::max(o_bm, alloc), o_ws + ws);
-    if (rc) return rc;
-    if (key_bytes) memcpy(sg.host, h_keys, key_bytes);
-    if (off_bytes) memcpy(sg.host + o_offs, h_offsets, off_bytes);
-    if (o_bm && hipMemcpyAsync(sg.dev, sg.host, o_bm, hipMemcpyHostToDevice, st) != hipSuccess)
-      return ADL_ERR_DEVICE;
-    rc = adl_bloom_build_device(sg.dev, h_offsets ? reinterpret_cast<uint64_t *>(sg.dev + o_offs) : nullptr,
-                                n, key_stride, bits_per_key, sg.dev + o_bm, sg.dev + o_ws, ws, st);
-    if (rc) {
-      (void)hipStreamSynchronize(st);
-      return rc;
-    }
-    if (hipMemcpyAsync(sg.host, sg.dev + o_bm, bytes, hipMemcpyDeviceToHost, st) != hipSuccess ||
-        hipStreamSynchronize(st) != hipSuccess)
-      return ADL_ERR_DEVICE;
-    memcpy(h_bitmap, sg.host, bytes);
-    return ADL_OK;
-  } catch (...) {
-    return ADL_ERR_DEVICE;
-  }
+  if (!h_bitmap || (n && !h_keys)) return ADL_ERR_INVALID_ARG;
+  if (!h_offsets && n && key_stride == 0) return ADL_ERR_INVALID_ARG;
+  if (!adl_host::bitmap_bytes(n, bits_per_key)) return bits_per_key < 0 ? ADL_ERR_INVALID_ARG : ADL_ERR_TOO_LARGE;
+  const uint64_t key_begin[2] = {0, n}, bitmap_off[1] = {0};
+  return adl_bloom_build_segmented(h_keys, h_offsets, key_stride, key_begin, 1, bits_per_key, h_bitmap, bitmap_off,
+                                   stream);
 }
 
 int adl_bloom_profile_enable(uint32_t capacity) {

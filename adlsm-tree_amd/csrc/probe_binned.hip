@@ -385,7 +385,10 @@ __global__ __launch_bounds__(kBlk) void pb_bin_kernel(const uint2 *__restrict__ 
                                                       const uint32_t *__restrict__ chunk_filter,
                                                       const uint32_t *__restrict__ scal, uint32_t k, uint32_t C,
                                                       uint32_t *__restrict__ ent, uint32_t *__restrict__ table,
-                                                      uint8_t *__restrict__ res) {
+                                                      uint8_t *__restrict__ res, uint32_t exp) {
+#ifndef ADL_BLOOM_STAMPS
+  exp = 0;  // diagnostics build only (wrong answers): 64 no entry stores, 128 no scatter (count only), 256 no count
+#endif
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   uint32_t *hist = lds;                          // kMaxTiles + 1 counters, later cursors
   uint32_t *scratch = lds + kMaxTiles + 4;       // scan scratch (64 words)
@@ -438,7 +441,7 @@ __global__ __launch_bounds__(kBlk) void pb_bin_kernel(const uint2 *__restrict__ 
 #pragma unroll
           for (int jj = 0; jj < KFIX; ++jj) {
             pos[r][jj] = fastmod(cur[r].x + (uint32_t)jj * cur[r].y, mod);
-            atomicAdd(&hist[pos[r][jj] >> kTL], 1u);
+            if (!(exp & 256)) atomicAdd(&hist[pos[r][jj] >> kTL], 1u);
           }
         } else {
           for (uint32_t jj = 0; jj < kk; ++jj) atomicAdd(&hist[fastmod(cur[r].x + jj * cur[r].y, mod) >> kTL], 1u);
@@ -453,7 +456,7 @@ __global__ __launch_bounds__(kBlk) void pb_bin_kernel(const uint2 *__restrict__ 
 #pragma unroll
     for (uint32_t r = 0; r < kCPT; ++r) {
       const uint32_t q = tid + r * kBlk;
-      if (live[r]) {
+      if (live[r] && !(exp & 128)) {
         if constexpr (KFIX > 0) {
           uint32_t sl[KFIX];
 #pragma unroll
@@ -474,6 +477,7 @@ __global__ __launch_bounds__(kBlk) void pb_bin_kernel(const uint2 *__restrict__ 
     const uint32_t nvec = total >> 2;
     const uint4 *src4 = reinterpret_cast<const uint4 *>(lpos);
     uint4 *dst4 = reinterpret_cast<uint4 *>(dst);
+    if (exp & 64) continue;
     for (uint32_t v = tid; v < nvec; v += kBlk) dst4[v] = src4[v];
     for (uint32_t v = (nvec << 2) + tid; v < total; v += kBlk) dst[v] = lpos[v];
   }
@@ -854,7 +858,7 @@ int adl_bloom_probe_batch_device(const uint8_t *d_keys, const uint64_t *d_offset
     if (int rc = adl_host::lds_limit<pb_tile_kernel>()) return rc;
     auto bin = [&](auto lim, auto kern) -> int {
       if (int rc = lim()) return rc;
-      hipLaunchKernelGGL(kern, dim3(cus), dim3(kBlk), lds_p1, st, hs, desc, cf, scal, p.k, p.C, ent, tab, res);
+      hipLaunchKernelGGL(kern, dim3(cus), dim3(kBlk), lds_p1, st, hs, desc, cf, scal, p.k, p.C, ent, tab, res, exp);
       ADL_HIP_TRY(hipGetLastError());
       hipLaunchKernelGGL(pb_tile_kernel, dim3(cus), dim3(kBlk), lds_p2, st, d_bitmaps, desc, F, scal, p.k, p.C, ent,
                          tab, res, exp);

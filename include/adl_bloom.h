@@ -120,7 +120,11 @@ int adl_bloom_build_segmented_device_ex(const uint8_t *d_keys, const uint64_t *d
 
 /* Host-pointer convenience: upload keys, build, download exactly
  * adl_bloom_bitmap_bytes(n, bpk) bytes into h_bitmap (which may be unaligned,
- * e.g. the tail of a std::string as in Keys2Block).  Synchronous. */
+ * e.g. the tail of a std::string as in Keys2Block).  Synchronous.  The same
+ * path as adl_bloom_build_segmented with one filter: pinned (hipHostMalloc'd /
+ * registered) key and bitmap buffers are DMAed directly, pageable ones staged
+ * through per-thread pinned buffers.  Replaces BloomFilter::Keys2Block
+ * (src/filter_block.cpp:9-33). */
 int adl_bloom_build(const uint8_t *h_keys, const uint64_t *h_offsets, uint64_t n,
                     uint32_t key_stride, int32_t bits_per_key, uint8_t *h_bitmap,
                     void *stream);

@@ -463,6 +463,28 @@ def test_host_api_build_and_probe(dev, ab, oracle):
     assert empty.size == 7 and not empty.any()
 
 
+@pytest.mark.parametrize("pinned", [False, True])
+def test_host_api_build_pinned_and_unaligned(dev, ab, oracle, pinned):
+    """adl_bloom_build takes the pipelined host path: pinned key and bitmap
+    buffers DMAed directly, pageable ones staged; the bitmap lands at an odd
+    address and nothing around it is written."""
+    n = 250_001
+    ref = oracle.splitmix_keys16(0x79, n)
+    if pinned:
+        kt = dev.empty((n, 16), dtype=dev.uint8).pin_memory()
+        keys = kt.numpy()
+        ot = dev.full((oracle.bitmap_bytes(n, 10) + 16,), 0xCD, dtype=dev.uint8).pin_memory()
+        buf = ot.numpy()
+    else:
+        keys = np.empty((n, 16), np.uint8)
+        buf = np.full(oracle.bitmap_bytes(n, 10) + 16, 0xCD, np.uint8)
+    keys[:] = ref
+    nb = oracle.bitmap_bytes(n, 10)
+    got = ab.build_host(keys, out=buf[3:3 + nb])
+    assert np.array_equal(got, oracle.keys2block(ref))
+    assert (buf[:3] == 0xCD).all() and (buf[3 + nb:] == 0xCD).all()
+
+
 def test_filter_set_resident_probe(dev, ab, oracle):
     bms = [oracle.keys2block(oracle.splitmix_keys16(200 + f, 5000 + f)) for f in range(4)]
     boff = np.concatenate([[0], np.cumsum([b.size for b in bms])]).astype(np.uint64)

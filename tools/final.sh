@@ -1,7 +1,8 @@
 #!/bin/bash
 # tools/final.sh -- one round's evidence in one GPU call: PMC passes (traffic +
 # integer issue) written into profiles/pmc_traffic.json first (bench.py reads
-# them), the GPU test suite, smoke(), the read-path latency bench, every bench
+# them), the GPU test suite, smoke(), the read-path latency bench, Gets beside
+# builds (readpath_test --coexist) and the server's tails, every bench
 # workload with CPU baselines, and rocprofv3 kernel traces of the headline and
 # var-len runs.
 set -u
@@ -20,6 +21,9 @@ timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('s
 tail -n 1 "$OUT/smoke.log"
 step readpath
 timeout -k 10 300 adlsm-tree_amd/bin/readpath_test --bench > "$OUT/readpath_bench.json" 2> "$OUT/readpath_bench.err" || exit 1
+step readpath_coexist_tails
+timeout -k 10 300 adlsm-tree_amd/bin/readpath_test --coexist 40 > "$OUT/coexist.json" 2> "$OUT/coexist.err" || exit 1
+timeout -k 10 200 adlsm-tree_amd/bin/readpath_test --tails 220000 > "$OUT/tails.json" 2> "$OUT/tails.err" || exit 1
 step sstable_pipebench
 for nt in "100000 8" "1000000 4"; do
   timeout -k 10 300 adlsm-tree_amd/bin/sstable_test pipebench $nt >> "$OUT/sstable_pipebench.jsonl" || exit 1
