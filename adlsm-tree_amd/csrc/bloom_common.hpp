@@ -200,7 +200,7 @@ struct Knobs {
   bool spin = true;               // ADL_BLOOM_SPIN: small cache probes watch their mapped answers
   bool probe_server = true;       // ADL_BLOOM_PROBE_SERVER: cache batches of <= 8 queries go to the server
   uint64_t server_idle_us = 2000;   // ADL_BLOOM_SERVER_IDLE_US
-  uint64_t server_life_us = 20000;  // ADL_BLOOM_SERVER_LIFE_US
+  uint64_t server_life_us = 1000000;  // ADL_BLOOM_SERVER_LIFE_US
   uint64_t pipe_mb = 128;         // ADL_BLOOM_PIPE_MB: keys per group of the pipelined host build
   bool debug = false;             // ADL_BLOOM_DEBUG: the plan and failing HIP calls to stderr
   uint32_t exp = 0, pb_exp = 0;   // ADL_BLOOM_EXP / ADL_PB_EXP: diagnostics build (make stamps) only
@@ -218,7 +218,7 @@ struct Knobs {
     spin = u64("ADL_BLOOM_SPIN", 1) != 0;
     probe_server = u64("ADL_BLOOM_PROBE_SERVER", 1) != 0;
     server_idle_us = u64("ADL_BLOOM_SERVER_IDLE_US", 2000);
-    server_life_us = u64("ADL_BLOOM_SERVER_LIFE_US", 20000);
+    server_life_us = u64("ADL_BLOOM_SERVER_LIFE_US", 1000000);
     pipe_mb = u64("ADL_BLOOM_PIPE_MB", 128);
     debug = u64("ADL_BLOOM_DEBUG", 0) != 0;
 #ifdef ADL_BLOOM_STAMPS

@@ -366,7 +366,10 @@ Server *create() {
   }
   for (hipEvent_t &e : s->exited)
     if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return fail();
-  // 100 MHz ticks: idle 2 ms, life 20 ms by default
+  // 100 MHz ticks: idle 2 ms, life 1 s by default.  (Life was 20 ms until
+  // round 5: under continuous Gets that relaunched the server 50 times a
+  // second, and a relaunch while a build runs waited 0.5-1.3 ms for the new
+  // wave to start: profiles/r05/r05m_coexist_life.txt.)
   s->idle_ticks = adl_host::knobs().server_idle_us * 100;
   s->life_ticks = adl_host::knobs().server_life_us * 100;
   std::lock_guard<std::mutex> g(g_reg_mu);
@@ -437,9 +440,13 @@ int probe(Server *s, const uint8_t *h_keys, const uint64_t *h_offsets, uint32_t 
   __atomic_store_n(&s->host->bell[my], seq, __ATOMIC_SEQ_CST);
   uint32_t bits = 0;
   bool done = false;
+  const auto tb = std::chrono::steady_clock::now();
+  bool relaunched = false;
   if (!__atomic_load_n(&s->host->ctl.alive, __ATOMIC_SEQ_CST)) {
     std::lock_guard<std::mutex> g(s->launch_mu);
+    const uint32_t gen0 = s->gen;
     if (int rc = ensure_running(s, my, seq, &bits, &done)) return rc;
+    relaunched = s->gen != gen0;
   }
   const auto t0 = std::chrono::steady_clock::now();
   auto since = [&] { return std::chrono::steady_clock::now() - t0; };
@@ -455,6 +462,15 @@ int probe(Server *s, const uint8_t *h_keys, const uint64_t *h_offsets, uint32_t 
       if (int rc = ensure_running(s, my, seq, &bits, &done)) return rc;
     }
     if (since() > kTimeout) return kBusy;
+  }
+  if (adl_host::knobs().debug) {
+    // ADL_BLOOM_DEBUG: where a slow request spent its time
+    const auto t1 = std::chrono::steady_clock::now();
+    const double us_ring = std::chrono::duration<double, std::micro>(t0 - tb).count();
+    const double us_wait = std::chrono::duration<double, std::micro>(t1 - t0).count();
+    if (us_ring + us_wait > 100.0)
+      fprintf(stderr, "adl_bloom server: slow request %.1f us (alive check / relaunch %.1f us%s, answer wait %.1f us)\n",
+              us_ring + us_wait, us_ring, relaunched ? ", relaunched" : "", us_wait);
   }
   for (uint64_t q = 0; q < n; ++q) h_out[q] = (uint8_t)((bits >> q) & 1u);
   return ADL_OK;

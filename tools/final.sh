@@ -23,7 +23,7 @@ step readpath
 timeout -k 10 300 adlsm-tree_amd/bin/readpath_test --bench > "$OUT/readpath_bench.json" 2> "$OUT/readpath_bench.err" || exit 1
 step readpath_coexist_tails
 timeout -k 10 300 adlsm-tree_amd/bin/readpath_test --coexist 40 > "$OUT/coexist.json" 2> "$OUT/coexist.err" || exit 1
-timeout -k 10 200 adlsm-tree_amd/bin/readpath_test --tails 220000 > "$OUT/tails.json" 2> "$OUT/tails.err" || exit 1
+ADL_BLOOM_SERVER_LIFE_US=20000 timeout -k 10 200 adlsm-tree_amd/bin/readpath_test --tails 220000 > "$OUT/tails.json" 2> "$OUT/tails.err" || exit 1
 step sstable_pipebench
 for nt in "100000 8" "1000000 4"; do
   timeout -k 10 300 adlsm-tree_amd/bin/sstable_test pipebench $nt >> "$OUT/sstable_pipebench.jsonl" || exit 1
