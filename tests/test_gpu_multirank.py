@@ -103,3 +103,76 @@ def test_two_ranks_one_gpu_compaction_and_probe_routing():
     assert out[0]["served"] + out[1]["served"] == 100_000_000
     assert out[0]["probe_sha"] == pins["probe"]["results_sha256"]
     assert out[0]["routed_sha"] == pins["probe"]["results_sha256"]
+
+
+def _rccl_worker(port, q):
+    """One rank on cuda:0 over backend "nccl" (RCCL on ROCm): the device-tensor
+    collectives bench.py and adlbloom.dist use at N > 1 -- the throughput
+    counters' SUM / MAX all-reduce, route_probe's three all-to-alls and
+    scatter_answers' SUM all-reduce of a uint8 vector -- run for real through
+    RCCL (world size 1: a single GPU box; the N > 1 run is the driver's)."""
+    import sys
+
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "adlsm-tree_amd"))
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import adlbloom as ab
+    import oracle as O
+    from adlbloom import dist as D
+
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                            device_id=torch.device("cuda:0"))
+    try:
+        res = {"backend": dist.get_backend()}
+        k = torch.tensor([3.0], dtype=torch.float64, device="cuda")
+        e = torch.tensor([0.25], dtype=torch.float64, device="cuda")
+        dist.all_reduce(k, op=dist.ReduceOp.SUM)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        res["reduce"] = [k.item(), e.item()]
+        T, per, n = 8, 20_000, 300_000
+        bms = [O.keys2block(O.splitmix_keys16(0x5EED + t, per)) for t in range(T)]
+        off = np.concatenate([[0], np.cumsum([b.size for b in bms])]).astype(np.uint64)
+        arena = np.concatenate(bms + [np.zeros(16, np.uint8)])
+        keys, fid, _ = O.synth_probe_queries(n, num_tables=T, keys_per_table=per)
+        want = O.probe_multi(keys, fid, arena, off)
+        d_arena = torch.from_numpy(arena).cuda()
+        d_off = torch.from_numpy(off.view(np.int64)).cuda()
+        own, lid = D.owner_table(T, 1)
+        own_t, lid_t = torch.from_numpy(own).cuda(), torch.from_numpy(lid).cuda()
+        probe_fn = lambda kk, ff: ab.probe_multi(kk, ff, d_arena, d_off)
+        stats = {}
+        got, served = D.route_probe(torch.from_numpy(keys).cuda(), torch.from_numpy(fid.view(np.int32)).cuda(),
+                                    own_t, lid_t, probe_fn, stats=stats)
+        res["routed_equal"] = bool(np.array_equal(got.cpu().numpy(), want))
+        res["served"] = served
+        idx = torch.arange(n, device="cuda")
+        full = D.scatter_answers(got, idx, n)
+        res["scatter_equal"] = bool(np.array_equal(full.cpu().numpy(), want))
+        q.put(res)
+    except Exception as ex:
+        q.put({"error": repr(ex)})
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rccl_world1_collectives():
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_worker, args=(_free_port(), q))
+    p.start()
+    res = q.get(timeout=200)
+    p.join(timeout=60)
+    assert "error" not in res, res
+    assert p.exitcode == 0
+    assert res["backend"] == "nccl"
+    assert res["reduce"] == [3.0, 0.25]
+    assert res["routed_equal"] and res["scatter_equal"]
+    assert res["served"] == 300_000
