@@ -366,7 +366,9 @@ __global__ __launch_bounds__(kBlk) void pb_scatter_kernel(const uint4 *__restric
   if (exp & 16) return;
   // run by run: consecutive lanes write consecutive slots (whole lines);
   // place by place (every lane of a store carrying one) measured the same
-  // (profiles/r04/probe_flat_k3.log)
+  // (profiles/r04/probe_flat_k3.log), and pieces of 64 slots dealt to the
+  // waves round robin (one search per piece) 61 % slower
+  // (profiles/r05/rejected/probe_k3_pieces.log)
   for (uint32_t f = wave; f < F; f += kBlk / kWave) {
     const uint32_t c = lcnt[f], lb = lbase[f], gs = lstart[f];
     for (uint32_t r = lane; r < c; r += kWave) hs[gs + r] = lhs[lb + r];
@@ -705,10 +707,11 @@ __global__ __launch_bounds__(kBlk) void pb_tile_kernel(const uint8_t *__restrict
 // ---------------------------------------------------------------- K6
 // Per block: the answers of its runs, gathered run by run into an LDS bit
 // array in the block's sorted order, then out[i] = the bit at the query's
-// place (coalesced).  Thread f takes filter f's run: its cleared bits are a
-// contiguous range of the answer array (filter order), read 32 at a time as
-// a funnel of two words and ORed into the LDS bits at the run's place: about
-// two loads per run instead of one per query, and no per-query search.
+// place (coalesced).  A filter's run of cleared bits is a contiguous range of
+// the answer array (filter order); the runs are cut into pieces of 32, and a
+// thread reads a piece as a funnel of two words and ORs it into the LDS bits
+// at the run's place: about two loads per 32 queries instead of one per
+// query, and one search per piece instead of one per query.
 // Small workgroups (kGatherBlk threads), so several blocks per CU overlap
 // their round trips.
 constexpr int kGatherBlk = 256;
@@ -721,7 +724,8 @@ __global__ __launch_bounds__(kGatherBlk) void pb_gather_kernel(const uint16_t *_
   constexpr uint32_t QPT = kQB / B;  // queries per thread
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   uint32_t *lbits = lds;  // kQB cleared bits in the block's sorted order
-  uint32_t *lcnt = lds + kQB / 32, *lstart = lcnt + F + 1, *lbase = lstart + F + 1, *scratch = lbase + F + 1;
+  uint32_t *lcnt = lds + kQB / 32, *lstart = lcnt + F + 1, *lbase = lstart + F + 1, *lpc = lbase + F + 1;
+  uint32_t *scratch = lpc + F + 1;
   const int tid = threadIdx.x;
   const uint32_t *clrw = reinterpret_cast<const uint32_t *>(res);
   // this thread's queries' places (coalesced 16-byte loads: 8 places each),
@@ -743,20 +747,28 @@ __global__ __launch_bounds__(kGatherBlk) void pb_gather_kernel(const uint16_t *_
   }
   for (uint32_t w = tid; w < kQB / 32; w += B) lbits[w] = 0u;
   load_runs<B>(cnt, start, blk, F, nullptr, lcnt, lstart, lbase, nullptr, scratch);
-  for (uint32_t f = tid; f < F; f += B) {
-    const uint32_t c = lcnt[f];
-    const uint32_t s0 = lstart[f], p0 = lbase[f];
-    for (uint32_t o = 0; o < c; o += 32) {
-      const uint32_t s = s0 + o, p = p0 + o, len = min(32u, c - o);
-      const uint32_t sh = s & 31u;
-      const uint32_t w0 = clrw[s >> 5], w1 = clrw[(s >> 5) + 1];  // (the array has 64 bytes of slack)
-      uint32_t v = sh ? (w0 >> sh) | (w1 << (32u - sh)) : w0;
-      if (len < 32) v &= (1u << len) - 1u;
-      if (!v) continue;
-      const uint32_t ps = p & 31u;
-      atomicOr(&lbits[p >> 5], v << ps);
-      if (ps && ps + len > 32) atomicOr(&lbits[(p >> 5) + 1], v >> (32u - ps));
+  // the runs cut into pieces of 32 queries, numbered over the block (one long
+  // run -- a batch with one filter -- spreads over all threads): lpc[f] = the
+  // first piece of filter f's run
+  for (uint32_t f = tid; f <= F; f += B) lpc[f] = f < F ? (lcnt[f] + 31u) >> 5 : 0u;
+  __syncthreads();
+  const uint32_t pieces = block_excl_scan_array<B>(lpc, F + 1, scratch);
+  for (uint32_t pc = tid; pc < pieces; pc += B) {
+    uint32_t lo = 0, hi = F;  // the last f with lpc[f] <= pc: its run holds piece pc
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (lpc[mid] <= pc) lo = mid; else hi = mid;
     }
+    const uint32_t o = (pc - lpc[lo]) * 32u;
+    const uint32_t s = lstart[lo] + o, p = lbase[lo] + o, len = min(32u, lcnt[lo] - o);
+    const uint32_t sh = s & 31u;
+    const uint32_t w0 = clrw[s >> 5], w1 = clrw[(s >> 5) + 1];  // (the array has 64 bytes of slack)
+    uint32_t v = sh ? (w0 >> sh) | (w1 << (32u - sh)) : w0;
+    if (len < 32) v &= (1u << len) - 1u;
+    if (!v) continue;
+    const uint32_t ps = p & 31u;
+    atomicOr(&lbits[p >> 5], v << ps);
+    if (ps && ps + len > 32) atomicOr(&lbits[(p >> 5) + 1], v >> (32u - ps));
   }
   __syncthreads();
 #pragma unroll
@@ -830,7 +842,7 @@ int adl_bloom_probe_batch_device(const uint8_t *d_keys, const uint64_t *d_offset
   const uint32_t cus = adl_host::device_cus();
   const size_t lds_k1 = (size_t)(2 * F + 2) * 4;                       // counters + tile counts
   const size_t lds_k3 = (size_t)(2 * kQB + 5 * (F + 1) + 32) * 4;      // hashes + 5 per-filter arrays + scratch
-  const size_t lds_k6 = (size_t)(kQB / 32 + 3 * (F + 1) + 32) * 4;     // answer bits + 3 per-filter arrays + scratch
+  const size_t lds_k6 = (size_t)(kQB / 32 + 4 * (F + 1) + 32) * 4;     // answer bits + 4 per-filter arrays + scratch
   const size_t lds_p1 = (size_t)(kMaxTiles + 4 + 64 + p.k * p.C) * 4;
   const size_t lds_p2 = (size_t)kTileBytes + 64 + (size_t)((F + 1 + 3) & ~3u) * 4 +
                         (size_t)(kBlk / kWave) * kMaskWords * 4;
