@@ -435,6 +435,32 @@ __global__ __launch_bounds__(kBlk) void pb_bin_kernel(const uint2 *__restrict__ 
 #pragma unroll
     for (uint32_t r = 0; r < kCPT; ++r) live[r] = live[r] && tid + r * kBlk < cnt;
     __syncthreads();
+    uint32_t *dst = ent + (uint64_t)c * k * C;
+    if (T == 1) {
+      // A filter of one tile (under 2^20 bits): the chunk's run is all of its
+      // entries, in query order -- no count, scan or atomics (a counting sort
+      // into one bucket serialises every wave's 64 atomics on one address).
+#pragma unroll
+      for (uint32_t r = 0; r < kCPT; ++r) {
+        if (live[r]) {
+          const uint32_t q = tid + r * kBlk;
+          for (uint32_t jj = 0; jj < kk; ++jj)
+            lpos[q * kk + jj] = (q << kTL) | (fastmod(cur[r].x + jj * cur[r].y, mod) & ((1u << kTL) - 1u));
+        }
+      }
+      const uint32_t total = cnt * kk;
+      if (tid == 0) {
+        table[d.table_base + j] = 0u;                 // tile 0 starts at 0
+        table[d.table_base + d.nchunks + j] = total;  // the row after the last tile: the total
+      }
+      __syncthreads();
+      const uint32_t nvec = total >> 2;
+      const uint4 *src4 = reinterpret_cast<const uint4 *>(lpos);
+      uint4 *dst4 = reinterpret_cast<uint4 *>(dst);
+      for (uint32_t v = tid; v < nvec; v += kBlk) dst4[v] = src4[v];
+      for (uint32_t v = (nvec << 2) + tid; v < total; v += kBlk) dst[v] = lpos[v];
+      continue;
+    }
     uint32_t pos[kCPT][KR];
 #pragma unroll
     for (uint32_t r = 0; r < kCPT; ++r) {
@@ -475,7 +501,6 @@ __global__ __launch_bounds__(kBlk) void pb_bin_kernel(const uint2 *__restrict__ 
       }
     }
     __syncthreads();
-    uint32_t *dst = ent + (uint64_t)c * k * C;
     const uint32_t nvec = total >> 2;
     const uint4 *src4 = reinterpret_cast<const uint4 *>(lpos);
     uint4 *dst4 = reinterpret_cast<uint4 *>(dst);
@@ -579,15 +604,32 @@ __global__ __launch_bounds__(kBlk) void pb_tile_kernel(const uint8_t *__restrict
   // bitmap, one tile ahead, so a tile starts with no table round trip.
   const uint32_t wv = __builtin_amdgcn_readfirstlane((uint32_t)wave);  // (SGPR: the stage cursor below is scalar)
   uint32_t pre_rs = 0, pre_re = 0;
+  // A tile of a filter with fewer chunks than waves would leave waves idle
+  // while a few process its long runs: each run is then cut into `split`
+  // equal parts (virtual runs v = jc * split + part), dealt to the waves like
+  // runs.  A wave flushes its mask at the end of each part, so parts of one
+  // chunk on several waves OR their cleared bits into the same words.
+  auto split_of = [](uint32_t nc) { return nc && nc < (uint32_t)NW ? (uint32_t)NW / nc : 1u; };
+  // virtual run v's (start, end) from the (tile, chunk) table row
+  // (split == 1, the common case, takes the plain row loads: no division)
+  auto vrun = [](const uint32_t *row, uint32_t nc, uint32_t split, uint32_t v, uint32_t &rs, uint32_t &re) {
+    if (split == 1) {
+      rs = row[v];
+      re = row[nc + v];
+      return;
+    }
+    const uint32_t jc = v / split, part = v - jc * split;
+    const uint32_t s0 = row[jc], e0 = row[nc + jc], len = e0 - s0;
+    rs = s0 + (len * part) / split;  // len < 2^16, part < split <= 16: no overflow
+    re = s0 + (len * (part + 1)) / split;
+  };
   auto prefetch_rows = [&](const TileRef &r) {
     const PFilter &dn = desc[r.f];
-    const uint32_t nc = dn.nchunks;
-    const uint32_t nq = nc > wv ? (nc - wv + NW - 1) / NW : 0u;
+    const uint32_t nc = dn.nchunks, split = split_of(nc), nvr = nc * split;
+    const uint32_t nq = nvr > wv ? (nvr - wv + NW - 1) / NW : 0u;
     if (nq) {
       const uint32_t *row = table + dn.table_base + (uint64_t)r.t * nc;
-      const uint32_t jc = wv + NW * min((uint32_t)lane, min((uint32_t)kWave, nq) - 1u);
-      pre_rs = row[jc];
-      pre_re = row[nc + jc];
+      vrun(row, nc, split, wv + NW * min((uint32_t)lane, min((uint32_t)kWave, nq) - 1u), pre_rs, pre_re);
     }
   };
   TileRef cur{};
@@ -614,10 +656,10 @@ __global__ __launch_bounds__(kBlk) void pb_tile_kernel(const uint8_t *__restrict
       prefetch_rows(cur);
     }
     const PFilter d = desc[now.f];
-    const uint32_t nc = d.nchunks;
+    const uint32_t nc = d.nchunks, split = split_of(nc), nvr = nc * split;
     const uint32_t *row = table + d.table_base + (uint64_t)now.t * nc;
-    // this wave's runs: chunks wave + NW*q; lane q holds run q's (start, end)
-    const uint32_t nq = nc > wv ? (nc - wv + NW - 1) / NW : 0u;
+    // this wave's (virtual) runs: wave + NW*q; lane q holds run q's (start, end)
+    const uint32_t nq = nvr > wv ? (nvr - wv + NW - 1) / NW : 0u;
     __syncthreads();  // the tile is in LDS
     // Two-stage pipeline over the wave's runs cut into stages of at most
     // kRunLoads x 64 entries (a long run is several stages): stage s+1's loads
@@ -667,11 +709,7 @@ __global__ __launch_bounds__(kBlk) void pb_tile_kernel(const uint8_t *__restrict
     for (uint32_t q0 = 0; q0 < nq; q0 += kWave) {
       const uint32_t nr = min((uint32_t)kWave, nq - q0);
       uint32_t rs = now_rs, re = now_re;  // the first 64 runs came with the tile
-      if (q0) {
-        const uint32_t jc = wv + NW * (q0 + min((uint32_t)lane, nr - 1u));
-        rs = row[jc];
-        re = row[nc + jc];
-      }
+      if (q0) vrun(row, nc, split, wv + NW * (q0 + min((uint32_t)lane, nr - 1u)), rs, re);
       // the stage cursor: run sq of this batch, entries from so
       uint32_t sq = 0, so = __builtin_amdgcn_readlane(rs, 0);
       auto take = [&](Stage &sg) {
@@ -679,7 +717,8 @@ __global__ __launch_bounds__(kBlk) void pb_tile_kernel(const uint8_t *__restrict
         const uint32_t qe = more ? __builtin_amdgcn_readlane(re, sq) : 0u;
         const uint32_t b0 = more ? so : 0u;
         const uint32_t b1 = more ? min(so + (uint32_t)(kRunLoads * kWave), qe) : 0u;
-        const uint32_t jc = wv + NW * (q0 + (more ? sq : nr - 1u));
+        const uint32_t v = wv + NW * (q0 + (more ? sq : nr - 1u));
+        const uint32_t jc = split == 1 ? v : v / split;  // the virtual run's chunk
         issue(sg, b0, b1, jc, more);
         if (more) {
           so = b1;

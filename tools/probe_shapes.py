@@ -24,7 +24,10 @@ torch.cuda.set_device(0)
 # (filters, keys per filter, queries, share of queries to filter 0 or None for uniform)
 SHAPES = [(1, 1_000_000, 20_000_000, None), (16, 1_000_000, 20_000_000, None), (256, 100_000, 20_000_000, None),
           (4096, 5_000, 20_000_000, None), (64, 300_000, 20_000_000, 0.9)]
-for F, per, n, skew in SHAPES:
+only = os.environ.get("PROBE_SHAPES")  # e.g. "3" or "0,3": indices into SHAPES
+for si, (F, per, n, skew) in enumerate(SHAPES):
+    if only and str(si) not in only.split(","):
+        continue
     keys_t = ab.synth_keys16(F * per, seed=0x5EED, device="cuda")
     kb = np.arange(F + 1, dtype=np.uint64) * per
     bms, boff, nbytes = ab.build_segmented(keys_t, kb)
