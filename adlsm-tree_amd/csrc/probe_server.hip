@@ -147,15 +147,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(16))) void probe
   const uint32_t lane = threadIdx.x;
   uint32_t served = __hip_atomic_load(&area->done[lane].seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   const uint64_t t0 = now_ticks();
-  uint64_t last = t0;
+  uint64_t last = t0, tprev = t0;
   bool closing = false;
   for (;;) {
+    const uint64_t tp = now_ticks();  // this poll (diagnostics: the gap since the previous one)
     const uint32_t bell = ld_sys(&area->bell[lane]);
     const bool pend = bell != served;
     const uint64_t pm = __ballot(pend);
     if (pm == 0) {
       if (closing) break;
-      const uint64_t t = now_ticks();
+      const uint64_t t = tp;
+      tprev = tp;
       const bool stop = __ballot(ld_sys(&area->ctl.stop[lane & 15]) != 0) != 0;
       if (stop || t - last > idle_ticks || t - t0 > life_ticks) {
         // Leaving: alive = 0 first, then one more poll, whose bells are
@@ -207,11 +209,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(16))) void probe
         const uint64_t word = (uint64_t)seq | ((uint64_t)((seq << 8) | bits) << 32);
         __hip_atomic_store(reinterpret_cast<uint64_t *>(&area->done[ju]), word, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_SYSTEM);
+        // diagnostics (read by the host under ADL_BLOOM_DEBUG): 10-ns ticks
+        // from the previous poll to the one that found the request, and from
+        // that poll to the answer
+        const uint64_t diag = (uint64_t)(uint32_t)(tp - tprev) | ((uint64_t)(uint32_t)(now_ticks() - tp) << 32);
+        __hip_atomic_store(reinterpret_cast<uint64_t *>(&area->done[ju].pad[0]), diag, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
       }
       __syncthreads();  // the group's LDS copy is read before the next group overwrites it
     }
     if (pend) served = bell;
     last = now_ticks();
+    tprev = tp;
     if (closing) break;
   }
   // the last poll's answers are out: the host may launch the next kernel (on
@@ -305,6 +314,10 @@ int ensure_running(Server *s, uint32_t my, uint32_t seq, uint32_t *bits, bool *d
         __builtin_ia32_pause();
         if (spin % 1024 == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(500)) {
           const hipError_t q = hipEventQuery(ev);
+          if (adl_host::knobs().debug)
+            fprintf(stderr, "adl_bloom server: generation %u not published after 500 us (gen_done %u, alive %u, event %d)\n",
+                    s->gen, __atomic_load_n(&s->host->ctl.gen_done, __ATOMIC_ACQUIRE),
+                    __atomic_load_n(&s->host->ctl.alive, __ATOMIC_ACQUIRE), (int)q);
           if (q == hipSuccess) break;
           if (q != hipErrorNotReady) {
             (void)hipGetLastError();
@@ -321,9 +334,19 @@ int ensure_running(Server *s, uint32_t my, uint32_t seq, uint32_t *bits, bool *d
   set_stop(s, 0);
   __atomic_store_n(&s->host->ctl.alive, 1u, __ATOMIC_SEQ_CST);
   const uint32_t gen = s->gen + 1;
+  const auto tl0 = std::chrono::steady_clock::now();
   hipLaunchKernelGGL(probe_server_kernel, dim3(1), dim3(64), 0, s->stream, s->dev, s->idle_ticks, s->life_ticks, gen);
+  const auto tl1 = std::chrono::steady_clock::now();
   if (hipGetLastError() != hipSuccess || hipEventRecord(s->exited[gen & 1], s->stream) != hipSuccess)
     return ADL_ERR_DEVICE;
+  if (adl_host::knobs().debug) {
+    const auto tl2 = std::chrono::steady_clock::now();
+    const double us_launch = std::chrono::duration<double, std::micro>(tl1 - tl0).count();
+    const double us_record = std::chrono::duration<double, std::micro>(tl2 - tl1).count();
+    if (us_launch + us_record > 50.0)
+      fprintf(stderr, "adl_bloom server: relaunch host calls: launch %.1f us, event record %.1f us\n", us_launch,
+              us_record);
+  }
   s->launched = true;
   s->gen = gen;
   g_launches.fetch_add(1, std::memory_order_relaxed);
@@ -468,9 +491,17 @@ int probe(Server *s, const uint8_t *h_keys, const uint64_t *h_offsets, uint32_t 
     const auto t1 = std::chrono::steady_clock::now();
     const double us_ring = std::chrono::duration<double, std::micro>(t0 - tb).count();
     const double us_wait = std::chrono::duration<double, std::micro>(t1 - t0).count();
-    if (us_ring + us_wait > 100.0)
-      fprintf(stderr, "adl_bloom server: slow request %.1f us (alive check / relaunch %.1f us%s, answer wait %.1f us)\n",
-              us_ring + us_wait, us_ring, relaunched ? ", relaunched" : "", us_wait);
+    if (us_ring + us_wait > 100.0) {
+      // the kernel's own view, stored after the answer: wait for it briefly
+      const auto tw = std::chrono::steady_clock::now();
+      while (std::chrono::steady_clock::now() - tw < std::chrono::microseconds(50)) __builtin_ia32_pause();
+      const uint64_t diag = __atomic_load_n(reinterpret_cast<const uint64_t *>(&s->host->done[my].pad[0]), __ATOMIC_ACQUIRE);
+      fprintf(stderr,
+              "adl_bloom server: slow request %.1f us (alive check / relaunch %.1f us%s, answer wait %.1f us; "
+              "kernel: %.2f us since its previous poll, %.2f us to answer)\n",
+              us_ring + us_wait, us_ring, relaunched ? ", relaunched" : "", us_wait, (double)(uint32_t)diag / 100.0,
+              (double)(uint32_t)(diag >> 32) / 100.0);
+    }
   }
   for (uint64_t q = 0; q < n; ++q) h_out[q] = (uint8_t)((bits >> q) & 1u);
   return ADL_OK;
