@@ -48,7 +48,9 @@
 
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
 #include <mutex>
+#include <thread>
 #include <new>
 #include <vector>
 
@@ -88,7 +90,8 @@ struct Ctl {
   uint32_t stop[16];  // replicated: lane l reads stop[l % 16] (a per-lane, vector load)
   uint32_t alive;     // host: 1 before a launch; kernel: 0 as it leaves (before its last poll)
   uint32_t gen_done;  // kernel: its launch generation, after its last poll's answers
-  uint32_t pad[14];
+  uint32_t gen_started;  // kernel: its launch generation, as it starts (after setting alive)
+  uint32_t pad[13];
 };
 
 // The shared area, one hipHostMalloc (mapped, coherent): bells, control, done
@@ -145,6 +148,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(16))) void probe
     Area *area, uint64_t idle_ticks, uint64_t life_ticks, uint32_t gen) {
   __shared__ __attribute__((aligned(16))) uint8_t lslot[kGroup][kSlotBytes];
   const uint32_t lane = threadIdx.x;
+  // a successor queued behind a running kernel (Server::launcher) announces
+  // itself: alive again, and its generation started
+  if (lane == 0) {
+    __hip_atomic_store(&area->ctl.alive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&area->ctl.gen_started, gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "");
   uint32_t served = __hip_atomic_load(&area->done[lane].seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   const uint64_t t0 = now_ticks();
   uint64_t last = t0, tprev = t0;
@@ -237,21 +247,32 @@ struct Server {
   Area *host = nullptr;  // mapped, coherent
   Area *dev = nullptr;   // its device address
   hipStream_t stream = nullptr;
-  // Completion events of the kernels, by generation parity: a relaunch is
-  // queued while its predecessor's dispatch may still be completing, and an
-  // event still pending must not be recorded again (that left
-  // hipStreamDestroy waiting at teardown now and then).  The kernel two
-  // generations back has completed before its successor started.
-  hipEvent_t exited[2] = {};
+  // Completion events of the kernels, by generation mod 3: with a successor
+  // queued behind the running kernel, the next launch re-records the event
+  // of the kernel two generations back, which completed before the running
+  // one started (an event still pending must not be recorded again: that left
+  // hipStreamDestroy waiting at teardown now and then).
+  static constexpr uint32_t kEvents = 3;
+  hipEvent_t exited[kEvents] = {};
   bool launched = false;
-  uint32_t gen = 0;  // the latest kernel's launch generation (Ctl::gen_done)
+  uint32_t gen = 0;  // the latest kernel's launch generation (Ctl::gen_done / gen_started)
   int device = 0;
-  std::mutex launch_mu;
+  std::mutex launch_mu;  // launches and gen
   std::mutex slot_mu[kSlots];
   uint32_t seq[kSlots] = {};
   std::atomic<uint32_t> next_slot{0};
   uint64_t id = 0;  // unique per server of this process (a thread's slot is per server)
   uint64_t idle_ticks = 0, life_ticks = 0;
+  // The launcher thread keeps one successor queued behind the running kernel
+  // while requests come in, so a kernel that reaches its life limit hands
+  // over to the next with no host call on any request's path (a launch call
+  // stalled 0.5 ms now and then: DESIGN.md §4).  Requests ask for a successor
+  // when none is queued; after a quiet period both kernels end on their idle
+  // limit and nothing is relaunched until the next request.
+  std::thread launcher;
+  std::mutex lmu;
+  std::condition_variable lcv;
+  bool want_successor = false, quit = false;
 };
 
 namespace {
@@ -267,14 +288,23 @@ std::vector<Server *> *g_reg = nullptr;
 
 void wait_all(Server *s) {
   if (!s->launched) return;
-  (void)hipEventSynchronize(s->exited[(s->gen + 1) & 1]);
-  (void)hipEventSynchronize(s->exited[s->gen & 1]);
+  for (uint32_t i = 0; i < Server::kEvents && i <= s->gen; ++i) (void)hipEventSynchronize(s->exited[(s->gen - i) % Server::kEvents]);
+}
+
+void stop_launcher(Server *s) {
+  {
+    std::lock_guard<std::mutex> g(s->lmu);
+    s->quit = true;
+  }
+  s->lcv.notify_one();
+  if (s->launcher.joinable()) s->launcher.join();
 }
 
 void stop_all_at_exit() {
   std::lock_guard<std::mutex> g(g_reg_mu);
   if (!g_reg) return;
   for (Server *s : *g_reg) {
+    stop_launcher(s);
     set_stop(s, 1);
     wait_all(s);
   }
@@ -287,19 +317,41 @@ bool answered(const Server *s, uint32_t my, uint32_t seq, uint32_t *bits) {
   return true;
 }
 
+// Launch generation s->gen + 1 behind whatever runs on the server's stream.
+// Caller holds launch_mu.
+int launch_next(Server *s) {
+  const uint32_t gen = s->gen + 1;
+  const auto tl0 = std::chrono::steady_clock::now();
+  hipLaunchKernelGGL(probe_server_kernel, dim3(1), dim3(64), 0, s->stream, s->dev, s->idle_ticks, s->life_ticks, gen);
+  const auto tl1 = std::chrono::steady_clock::now();
+  if (hipGetLastError() != hipSuccess || hipEventRecord(s->exited[gen % Server::kEvents], s->stream) != hipSuccess)
+    return ADL_ERR_DEVICE;
+  if (adl_host::knobs().debug) {
+    const double us_launch = std::chrono::duration<double, std::micro>(tl1 - tl0).count();
+    if (us_launch > 50.0) fprintf(stderr, "adl_bloom server: launch call of generation %u took %.1f us\n", gen, us_launch);
+  }
+  s->launched = true;
+  s->gen = gen;
+  g_launches.fetch_add(1, std::memory_order_relaxed);
+  return ADL_OK;
+}
+
 // The caller saw alive == 0 after ringing bell `my` (or waited long): make
-// sure a kernel will answer it.  Caller holds launch_mu.  A kernel that
-// cleared alive is in its last poll or gone: wait until it has published its
-// generation (its last answers are out by then; no wait for its completion
-// event), then launch the next one unless that last poll answered the
-// request.  *done = answered.
+// sure a kernel will answer it.  Caller holds launch_mu.
+//  * a launched kernel has not started yet (a queued successor, or a fresh
+//    launch): it will poll the bell;
+//  * the last launched kernel runs and alive is 1: it will poll the bell,
+//    unless it has failed (its completion event says so);
+//  * it cleared alive: it is in its last poll or gone: wait until it has
+//    published its generation (its last answers are out by then), then
+//    launch the next one unless that last poll answered the request.
+// *done = answered.
 int ensure_running(Server *s, uint32_t my, uint32_t seq, uint32_t *bits, bool *done) {
   *done = false;
   if (s->launched) {
-    hipEvent_t ev = s->exited[s->gen & 1];
+    if (__atomic_load_n(&s->host->ctl.gen_started, __ATOMIC_SEQ_CST) != s->gen) return ADL_OK;
+    hipEvent_t ev = s->exited[s->gen % Server::kEvents];
     if (__atomic_load_n(&s->host->ctl.alive, __ATOMIC_SEQ_CST)) {
-      // alive: a kernel launched since (or not yet started) will poll the bell,
-      // unless it has failed
       const hipError_t q = hipEventQuery(ev);
       if (q == hipErrorNotReady) return ADL_OK;
       if (q != hipSuccess) {
@@ -314,10 +366,6 @@ int ensure_running(Server *s, uint32_t my, uint32_t seq, uint32_t *bits, bool *d
         __builtin_ia32_pause();
         if (spin % 1024 == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(500)) {
           const hipError_t q = hipEventQuery(ev);
-          if (adl_host::knobs().debug)
-            fprintf(stderr, "adl_bloom server: generation %u not published after 500 us (gen_done %u, alive %u, event %d)\n",
-                    s->gen, __atomic_load_n(&s->host->ctl.gen_done, __ATOMIC_ACQUIRE),
-                    __atomic_load_n(&s->host->ctl.alive, __ATOMIC_ACQUIRE), (int)q);
           if (q == hipSuccess) break;
           if (q != hipErrorNotReady) {
             (void)hipGetLastError();
@@ -333,24 +381,29 @@ int ensure_running(Server *s, uint32_t my, uint32_t seq, uint32_t *bits, bool *d
   }
   set_stop(s, 0);
   __atomic_store_n(&s->host->ctl.alive, 1u, __ATOMIC_SEQ_CST);
-  const uint32_t gen = s->gen + 1;
-  const auto tl0 = std::chrono::steady_clock::now();
-  hipLaunchKernelGGL(probe_server_kernel, dim3(1), dim3(64), 0, s->stream, s->dev, s->idle_ticks, s->life_ticks, gen);
-  const auto tl1 = std::chrono::steady_clock::now();
-  if (hipGetLastError() != hipSuccess || hipEventRecord(s->exited[gen & 1], s->stream) != hipSuccess)
-    return ADL_ERR_DEVICE;
-  if (adl_host::knobs().debug) {
-    const auto tl2 = std::chrono::steady_clock::now();
-    const double us_launch = std::chrono::duration<double, std::micro>(tl1 - tl0).count();
-    const double us_record = std::chrono::duration<double, std::micro>(tl2 - tl1).count();
-    if (us_launch + us_record > 50.0)
-      fprintf(stderr, "adl_bloom server: relaunch host calls: launch %.1f us, event record %.1f us\n", us_launch,
-              us_record);
+  return launch_next(s);
+}
+
+// Launcher thread: on request, queue a successor behind the running kernel
+// when none is queued (the last launched kernel has started) and the server
+// is not being stopped.
+void launcher_main(Server *s) {
+  (void)hipSetDevice(s->device);
+  std::unique_lock<std::mutex> lk(s->lmu);
+  for (;;) {
+    s->lcv.wait(lk, [&] { return s->want_successor || s->quit; });
+    if (s->quit) return;
+    s->want_successor = false;
+    lk.unlock();
+    {
+      std::lock_guard<std::mutex> g(s->launch_mu);
+      const bool stopping = __atomic_load_n(&s->host->ctl.stop[0], __ATOMIC_SEQ_CST) != 0;
+      if (s->launched && !stopping && __atomic_load_n(&s->host->ctl.gen_started, __ATOMIC_SEQ_CST) == s->gen &&
+          __atomic_load_n(&s->host->ctl.gen_done, __ATOMIC_SEQ_CST) != s->gen)
+        (void)launch_next(s);  // a failure shows on the request path (its event)
+    }
+    lk.lock();
   }
-  s->launched = true;
-  s->gen = gen;
-  g_launches.fetch_add(1, std::memory_order_relaxed);
-  return ADL_OK;
 }
 
 }  // namespace
@@ -395,6 +448,11 @@ Server *create() {
   // wave to start: profiles/r05/r05m_coexist_life.txt.)
   s->idle_ticks = adl_host::knobs().server_idle_us * 100;
   s->life_ticks = adl_host::knobs().server_life_us * 100;
+  try {
+    s->launcher = std::thread(launcher_main, s);
+  } catch (...) {
+    return fail();
+  }
   std::lock_guard<std::mutex> g(g_reg_mu);
   if (!g_reg) {
     g_reg = new std::vector<Server *>;
@@ -414,6 +472,7 @@ void destroy(Server *s) {
         break;
       }
   }
+  stop_launcher(s);
   set_stop(s, 1);
   wait_all(s);
   (void)hipStreamSynchronize(s->stream);
@@ -502,6 +561,16 @@ int probe(Server *s, const uint8_t *h_keys, const uint64_t *h_offsets, uint32_t 
               us_ring + us_wait, us_ring, relaunched ? ", relaunched" : "", us_wait, (double)(uint32_t)diag / 100.0,
               (double)(uint32_t)(diag >> 32) / 100.0);
     }
+  }
+  // no successor queued behind the running kernel (the last launched one has
+  // started and not exited): ask the launcher for one, off this request's path
+  if (__atomic_load_n(&s->host->ctl.gen_started, __ATOMIC_RELAXED) == __atomic_load_n(&s->gen, __ATOMIC_RELAXED) &&
+      __atomic_load_n(&s->host->ctl.gen_done, __ATOMIC_RELAXED) != __atomic_load_n(&s->gen, __ATOMIC_RELAXED)) {
+    {
+      std::lock_guard<std::mutex> g(s->lmu);
+      s->want_successor = true;
+    }
+    s->lcv.notify_one();
   }
   for (uint64_t q = 0; q < n; ++q) h_out[q] = (uint8_t)((bits >> q) & 1u);
   return ADL_OK;
