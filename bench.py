@@ -649,6 +649,11 @@ def lds_roofline(workload, kernels_us):
         return None
     out = {"source": "profiles/pmc_traffic.json (SQ_LDS_IDX_ACTIVE, SQ_LDS_BANK_CONFLICT, GRBM_GUI_ACTIVE)",
            "model": "array cycles summed over 256 CUs; busy = cycles / (256 x kernel cycles)"}
+    if workload == "single":
+        # the bound measured directly: the same pass A
+        # with a conflict-free counting sort (diagnostics build, wrong tiles)
+        out["conflict_free_pass_a_us"] = {"real_sort": 101.0, "conflict_free": 97.7, "gain_frac": 0.034,
+                                          "source": "profiles/r05/r05b_lds_conflict_free_ab.log"}
     for k, v in e.items():
         us = kernels_us.get(k)
         clk = v.get("clock_ghz") or 2.4
