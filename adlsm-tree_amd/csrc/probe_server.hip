@@ -255,7 +255,8 @@ struct Server {
   static constexpr uint32_t kEvents = 3;
   hipEvent_t exited[kEvents] = {};
   bool launched = false;
-  uint32_t gen = 0;  // the latest kernel's launch generation (Ctl::gen_done / gen_started)
+  uint32_t gen = 0;  // the latest kernel's launch generation (Ctl::gen_done / gen_started); launch_mu
+  std::atomic<uint32_t> gen_pub{0};  // the same, for lock-free readers (probe's successor check)
   int device = 0;
   std::mutex launch_mu;  // launches and gen
   std::mutex slot_mu[kSlots];
@@ -332,6 +333,7 @@ int launch_next(Server *s) {
   }
   s->launched = true;
   s->gen = gen;
+  s->gen_pub.store(gen, std::memory_order_release);
   g_launches.fetch_add(1, std::memory_order_relaxed);
   return ADL_OK;
 }
@@ -564,8 +566,9 @@ int probe(Server *s, const uint8_t *h_keys, const uint64_t *h_offsets, uint32_t 
   }
   // no successor queued behind the running kernel (the last launched one has
   // started and not exited): ask the launcher for one, off this request's path
-  if (__atomic_load_n(&s->host->ctl.gen_started, __ATOMIC_RELAXED) == __atomic_load_n(&s->gen, __ATOMIC_RELAXED) &&
-      __atomic_load_n(&s->host->ctl.gen_done, __ATOMIC_RELAXED) != __atomic_load_n(&s->gen, __ATOMIC_RELAXED)) {
+  const uint32_t g_last = s->gen_pub.load(std::memory_order_acquire);
+  if (g_last && __atomic_load_n(&s->host->ctl.gen_started, __ATOMIC_RELAXED) == g_last &&
+      __atomic_load_n(&s->host->ctl.gen_done, __ATOMIC_RELAXED) != g_last) {
     {
       std::lock_guard<std::mutex> g(s->lmu);
       s->want_successor = true;
