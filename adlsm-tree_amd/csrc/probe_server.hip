@@ -351,8 +351,14 @@ int launch_next(Server *s) {
 int ensure_running(Server *s, uint32_t my, uint32_t seq, uint32_t *bits, bool *done) {
   *done = false;
   if (s->launched) {
-    if (__atomic_load_n(&s->host->ctl.gen_started, __ATOMIC_SEQ_CST) != s->gen) return ADL_OK;
     hipEvent_t ev = s->exited[s->gen % Server::kEvents];
+    if (__atomic_load_n(&s->host->ctl.gen_started, __ATOMIC_SEQ_CST) != s->gen) {
+      // not started yet, unless it failed (then its completion event says so)
+      const hipError_t q = hipEventQuery(ev);
+      if (q == hipSuccess || q == hipErrorNotReady) return ADL_OK;
+      (void)hipGetLastError();
+      return ADL_ERR_DEVICE;
+    }
     if (__atomic_load_n(&s->host->ctl.alive, __ATOMIC_SEQ_CST)) {
       const hipError_t q = hipEventQuery(ev);
       if (q == hipErrorNotReady) return ADL_OK;
