@@ -8,7 +8,7 @@ slowest rank's time here bounds the N-GPU step from below (the node's own
 effects -- clocks, the host, the final 16-byte all-reduce -- are the driver's
 SCALE run to show).  One JSON line per (workload, N, rank).
 
-usage: python tools/shard_times.py [steps]
+usage: [SHARD_KINDS=compaction,probe] [SHARD_NS=1,2,4,8] python tools/shard_times.py [steps]
 """
 import json
 import os
@@ -24,8 +24,10 @@ import bench  # noqa: E402
 
 steps = int(sys.argv[1]) if len(sys.argv) > 1 else 10
 torch.cuda.set_device(0)
-for kind in ("compaction", "probe"):
-    for N in (1, 2, 4, 8):
+kinds = os.environ.get("SHARD_KINDS", "compaction,probe").split(",")
+ns = [int(x) for x in os.environ.get("SHARD_NS", "1,2,4,8").split(",")]
+for kind in kinds:
+    for N in ns:
         for rank in sorted({0, N - 1}):
             w = bench.Workload(kind, rank, 0, N, 100_000_000 if kind == "probe" else 0)
             if kind == "probe":
