@@ -61,6 +61,7 @@ constexpr uint32_t kSentinel = 0xFFFFFFFFu;
 constexpr uint16_t kNoSlot = 0xFFFF;            // a query that is answered 0 without probing
 constexpr uint32_t kLdsWords = 40960;           // 160 KiB
 constexpr uint64_t kMinBinned = 1ull << 20;     // below this the direct kernel wins
+constexpr uint32_t kMaxSlots = 1024;            // pb_tile workgroups (the tile split's slots)
 
 struct PFilter {
   uint32_t m, magic, shift, tiles;
@@ -81,7 +82,7 @@ struct Plan {
   uint64_t maxch = 0;
   // workspace byte offsets
   uint32_t ng = 0;  // groups of kScanGroup blocks (K2)
-  uint64_t o_desc, o_scal, o_cnt, o_start, o_gsum, o_cf, o_dest, o_hs, o_ent, o_tab, o_res, total;
+  uint64_t o_desc, o_scal, o_cnt, o_start, o_gsum, o_cf, o_dest, o_hs, o_ent, o_tab, o_split, o_res, total;
 };
 
 constexpr uint32_t kScanGroup = 64;  // blocks per column-sum group (K2)
@@ -113,6 +114,7 @@ Plan make_plan(uint64_t n, uint32_t F, int32_t bpk) {
   p.o_hs = take(n * 8);
   p.o_ent = take(p.maxch * p.k * p.C * 4);
   p.o_tab = take(p.maxch * (kMaxTiles + 1) * 4);
+  p.o_split = take((kMaxSlots + 1) * 4);
   p.o_res = take(n + 64);
   p.total = o;
   return p;
@@ -211,12 +213,23 @@ __global__ __launch_bounds__(kBlk) void pb_colsum_kernel(const uint32_t *__restr
   }
 }
 
+// The tile split for pb_tile's G workgroups: slot s takes global tiles
+// [split[s], split[s+1]), a contiguous range holding about 1/G of the work.  A
+// tile's work is its bitmap load plus its entries (kTileWork + k x its
+// filter's queries / tiles, in 4-byte units): splitting by tile count would
+// put several tiles of a hot filter on one workgroup (64 filters with 90 % of
+// the queries on one: 1.0 -> 5.5 ms), splitting by work gives a hot tile a
+// workgroup of its own (and the workgroups after it none).
+constexpr uint64_t kTileWork = kTileBytes / 4;
+
 __global__ __launch_bounds__(kBlk) void pb_plan_kernel(uint32_t *__restrict__ gsum, uint32_t ng, uint32_t F,
                                                        uint32_t C, uint64_t maxch, PFilter *__restrict__ desc,
                                                        uint32_t *__restrict__ chunk_filter,
-                                                       uint32_t *__restrict__ scal) {
+                                                       uint32_t *__restrict__ scal, uint32_t k, uint32_t G,
+                                                       uint32_t *__restrict__ split) {
   __shared__ uint32_t scratch[kBlk / kWave + 1];
   __shared__ uint64_t red[kBlk / kWave];
+  __shared__ uint32_t ltb[kMaxBucketFilters + 1], lq[kMaxBucketFilters + 1];  // tile_base, qbase
   const uint64_t stride = F + 1;
   uint64_t cq = 0, cc = 0, ct = 0;  // running query / chunk / table-entry starts over filter blocks
   for (uint32_t f0 = 0; f0 <= F; f0 += kBlk) {
@@ -260,6 +273,8 @@ __global__ __launch_bounds__(kBlk) void pb_plan_kernel(uint32_t *__restrict__ gs
     }
     __syncthreads();
     if (f <= F) {
+      ltb[f] = desc[f].tile_base;
+      lq[f] = (uint32_t)(cq + pq);
       desc[f].cnt = tot;
       desc[f].qbase = (uint32_t)(cq + pq);
       desc[f].chunk_base = (uint32_t)(cc + pc);
@@ -274,6 +289,33 @@ __global__ __launch_bounds__(kBlk) void pb_plan_kernel(uint32_t *__restrict__ gs
   }
   __syncthreads();
   for (uint64_t j = cc + threadIdx.x; j < maxch; j += kBlk) chunk_filter[j] = kSentinel;
+  // the work before tile t of filter f (filters in order, a filter's queries
+  // spread evenly over its tiles)
+  auto work = [&](uint32_t f, uint32_t t) -> uint64_t {
+    const uint32_t tiles = ltb[f + 1] - ltb[f], q = lq[f + 1] - lq[f];
+    return kTileWork * (ltb[f] + t) + (uint64_t)k * (lq[f] + (tiles ? (uint64_t)t * q / tiles : 0u));
+  };
+  const uint64_t wtot = work(F, 0);  // (filter F, the out-of-range bucket, has no tiles)
+  for (uint32_t s = threadIdx.x; s <= G; s += kBlk) {
+    uint32_t g = 0;  // the first tile whose work starts at or after s / G of the total
+    if (s == G) {
+      g = ltb[F];
+    } else if (s && wtot) {
+      const uint64_t target = ((uint64_t)s * wtot + G - 1) / G;  // >= 1
+      uint32_t lo = 0, hi = F;  // work(lo, 0) < target <= work(hi, 0)
+      while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (work(mid, 0) < target) lo = mid; else hi = mid;
+      }
+      uint32_t tl = 0, th = ltb[lo + 1] - ltb[lo];  // work(lo, tl) < target <= work(lo, th)
+      while (th - tl > 1) {
+        const uint32_t mid = (tl + th) >> 1;
+        if (work(lo, mid) < target) tl = mid; else th = mid;
+      }
+      g = ltb[lo] + th;
+    }
+    split[s] = g;
+  }
 }
 
 __global__ __launch_bounds__(kBlk) void pb_starts_kernel(const uint32_t *__restrict__ cnt,
@@ -518,7 +560,8 @@ __global__ __launch_bounds__(kBlk) void pb_bin_kernel(const uint2 *__restrict__ 
 constexpr uint32_t kTileVecPT = kTileBytes / 16 / kBlk;  // 16-byte tile vectors per thread
 constexpr int kRunLoads = 6;                             // entries per run per stage: 6 x 64 (runs average ~320)
 constexpr uint32_t kMaskW64 = (kMaxC + 63) / 64 + 1;     // a wave's cleared-bit mask of one chunk (+ its shift), u64 words
-constexpr uint32_t kMaskWords = 2 * kMaskW64;
+constexpr int kRegRuns = 8;                               // runs per wave whose masks accumulate over a filter's tiles
+constexpr uint32_t kMaskWords = 2 * kMaskW64 + 2 * kRegRuns;  // + word 64 of each accumulated mask
 
 struct TileRef {
   uint32_t f, t, sh, nvec, tail;
@@ -550,6 +593,7 @@ __global__ __launch_bounds__(kBlk) void pb_tile_kernel(const uint8_t *__restrict
                                                        const uint32_t *__restrict__ scal, uint32_t k, uint32_t C,
                                                        const uint32_t *__restrict__ ent,
                                                        const uint32_t *__restrict__ table,
+                                                       const uint32_t *__restrict__ split,
                                                        uint8_t *__restrict__ res, uint32_t exp) {
 #ifndef ADL_BLOOM_STAMPS
   exp = 0;  // diagnostics build only (wrong answers): 1 no answer stores, 2 no bitmap loads, 4 no entry loads
@@ -560,17 +604,24 @@ __global__ __launch_bounds__(kBlk) void pb_tile_kernel(const uint8_t *__restrict
   const int tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid / kWave;
   // A clear bit sets its query's "cleared" bit.  Each wave gathers the bits
   // of the run (one chunk) it is testing in a private LDS mask of the chunk's
-  // 4 096 slots (shifted by the chunk's first slot mod 64), and ORs the mask's
-  // nonzero 64-bit words into the global bit array with coalesced
-  // device-scope atomics when it moves to its next run: one or two atomic
-  // wave-instructions per run (65 words) instead of ~1 200 scattered byte
-  // stores.  The flush is issued after a stage's tests and before the next
-  // stage's loads, so only the wait for the stage already in flight can
-  // include it.
+  // 4 096 slots (shifted by the chunk's first slot mod 64).  When the wave
+  // moves to its next run, the mask goes into the wave's registers: lane l
+  // holds word l of the masks of the wave's first kRegRuns runs (the same
+  // chunks in every tile of a filter, since a workgroup takes a contiguous
+  // range of tiles, mostly of one filter).  The registers are ORed into the
+  // global bit array with coalesced 64-bit device-scope atomics only when the
+  // workgroup moves on to another filter: about one flush per chunk and
+  // workgroup instead of one per (tile, chunk) run (round 5: the run-by-run
+  // flushes were ~1 GB of memory-side atomic traffic per 100 M queries).
+  // Runs past the first kRegRuns of a wave flush at their end as before.
   unsigned long long *clr64 = reinterpret_cast<unsigned long long *>(res);  // (the workspace area is 256-B aligned)
   uint32_t *zmaskw = lds + (kTileBytes + 64) / 4 + ((F + 1 + 3) & ~3u) + (uint32_t)wave * kMaskWords;  // 8-B aligned
   unsigned long long *zmask64 = reinterpret_cast<unsigned long long *>(zmaskw);
   for (uint32_t w = (uint32_t)lane; w < kMaskWords; w += kWave) zmaskw[w] = 0u;
+  unsigned long long rmask[kRegRuns];  // lane l: word l of run slot i's mask
+  unsigned long long *rmx = zmask64 + kMaskW64;  // word 64 of run slot i's mask (LDS, lane 0)
+#pragma unroll
+  for (int i = 0; i < kRegRuns; ++i) rmask[i] = 0ull;
   auto flush_run = [&](uint32_t rq) {
 #pragma unroll
     for (uint32_t k2 = 0; k2 < 2; ++k2) {
@@ -585,7 +636,6 @@ __global__ __launch_bounds__(kBlk) void pb_tile_kernel(const uint8_t *__restrict
     }
   };
   constexpr int NW = kBlk / kWave;
-  const uint32_t total_tiles = scal[0];
   for (uint32_t f = tid; f <= F; f += kBlk) ltb[f] = desc[f].tile_base;
   __syncthreads();
   const uint32_t G = gridDim.x;
@@ -632,13 +682,53 @@ __global__ __launch_bounds__(kBlk) void pb_tile_kernel(const uint8_t *__restrict
       vrun(row, nc, split, wv + NW * min((uint32_t)lane, min((uint32_t)kWave, nq) - 1u), pre_rs, pre_re);
     }
   };
+  // this workgroup's tiles: a contiguous range of about 1/G of the work
+  // (pb_plan's split; mostly one filter's tiles, so the register masks above
+  // accumulate over all of them)
+  const uint32_t gb = split[slot], ge = split[slot + 1];
+  // the filter whose chunks the register masks hold, and what locates them
+  uint32_t mf = ~0u, m_qbase = 0, m_split = 1, m_nq = 0;
+  auto flush_regs = [&]() {
+#pragma unroll
+    for (int i = 0; i < kRegRuns; ++i) {
+      if ((uint32_t)i < m_nq) {
+        const uint32_t v = wv + NW * (uint32_t)i;
+        const uint32_t jc = m_split == 1 ? v : v / m_split;
+        const uint32_t rq = m_qbase + jc * C;
+        if (rmask[i]) atomicOr(&clr64[(rq >> 6) + lane], rmask[i]);
+        if (lane == 0 && rmx[i]) {
+          atomicOr(&clr64[(rq >> 6) + kWave], rmx[i]);
+          rmx[i] = 0ull;
+        }
+      }
+      rmask[i] = 0ull;
+    }
+  };
+  // the run in slot qi of this wave ends: its LDS mask into the registers (or,
+  // past the register slots, straight to the global array)
+  auto retire_run = [&](uint32_t qi, uint32_t rq) {
+    if (qi >= (uint32_t)kRegRuns) {
+      flush_run(rq);
+      return;
+    }
+    const unsigned long long v = zmask64[lane];
+    zmask64[lane] = 0ull;
+    if (lane == 0) {
+      rmx[qi] |= zmask64[kWave];
+      zmask64[kWave] = 0ull;
+    }
+#pragma unroll
+    for (int i = 0; i < kRegRuns; ++i)
+      if ((uint32_t)i == qi) rmask[i] |= v;
+  };
+  static_assert(kMaskW64 == kWave + 1, "a chunk mask is kWave words plus one");
   TileRef cur{};
-  if (slot < total_tiles) {
-    cur = tile_ref(desc, ltb, F, slot);
+  if (gb < ge) {
+    cur = tile_ref(desc, ltb, F, gb);
     prefetch(cur);
     prefetch_rows(cur);
   }
-  for (uint32_t g = slot; g < total_tiles; g += G) {
+  for (uint32_t g = gb; g < ge; ++g) {
     __syncthreads();  // the previous tile's lookups are done
     uint4 *l4 = reinterpret_cast<uint4 *>(ltile);
 #pragma unroll
@@ -650,8 +740,8 @@ __global__ __launch_bounds__(kBlk) void pb_tile_kernel(const uint8_t *__restrict
       reinterpret_cast<uint8_t *>(ltile)[cur.nvec * 16 + tid] = bitmaps[cur.a0 + cur.nvec * 16 + tid];
     const TileRef now = cur;
     const uint32_t now_rs = pre_rs, now_re = pre_re;
-    if (g + G < total_tiles) {
-      cur = tile_ref(desc, ltb, F, g + G);
+    if (g + 1 < ge) {
+      cur = tile_ref(desc, ltb, F, g + 1);
       prefetch(cur);
       prefetch_rows(cur);
     }
@@ -660,6 +750,13 @@ __global__ __launch_bounds__(kBlk) void pb_tile_kernel(const uint8_t *__restrict
     const uint32_t *row = table + d.table_base + (uint64_t)now.t * nc;
     // this wave's (virtual) runs: wave + NW*q; lane q holds run q's (start, end)
     const uint32_t nq = nvr > wv ? (nvr - wv + NW - 1) / NW : 0u;
+    if (now.f != mf) {  // (wave-uniform) a new filter: the previous one's masks out
+      flush_regs();
+      mf = now.f;
+      m_qbase = d.qbase;
+      m_split = split;
+      m_nq = nq;
+    }
     __syncthreads();  // the tile is in LDS
     // Two-stage pipeline over the wave's runs cut into stages of at most
     // kRunLoads x 64 entries (a long run is several stages): stage s+1's loads
@@ -668,14 +765,15 @@ __global__ __launch_bounds__(kBlk) void pb_tile_kernel(const uint8_t *__restrict
     // entry -- so the compiler can count them and wait for one stage only.
     struct Stage {
       uint32_t x[kRunLoads];
-      uint32_t b0, b1, jc;
+      uint32_t b0, b1, jc, qi;  // qi: the run's slot in this wave's list
       bool live;  // a stage of a run (possibly empty); false past the batch's last run
     };
-    auto issue = [&](Stage &sg, uint32_t b0, uint32_t b1, uint32_t jc, bool live) {
+    auto issue = [&](Stage &sg, uint32_t b0, uint32_t b1, uint32_t jc, uint32_t qi, bool live) {
       sg.live = live;
       sg.b0 = b0;
       sg.b1 = b1;
       sg.jc = jc;
+      sg.qi = qi;
       const uint32_t *run = ent + (uint64_t)(d.chunk_base + jc) * k * C;
 #pragma unroll
       for (int u = 0; u < kRunLoads; ++u) {
@@ -704,7 +802,7 @@ __global__ __launch_bounds__(kBlk) void pb_tile_kernel(const uint8_t *__restrict
         }
       }
       // the run ends here: the next stage is another run's, or past the last
-      if (sg.live && (!nx.live || nx.jc != sg.jc)) flush_run(rq);
+      if (sg.live && (!nx.live || nx.qi != sg.qi)) retire_run(sg.qi, rq);
     };
     for (uint32_t q0 = 0; q0 < nq; q0 += kWave) {
       const uint32_t nr = min((uint32_t)kWave, nq - q0);
@@ -717,9 +815,10 @@ __global__ __launch_bounds__(kBlk) void pb_tile_kernel(const uint8_t *__restrict
         const uint32_t qe = more ? __builtin_amdgcn_readlane(re, sq) : 0u;
         const uint32_t b0 = more ? so : 0u;
         const uint32_t b1 = more ? min(so + (uint32_t)(kRunLoads * kWave), qe) : 0u;
-        const uint32_t v = wv + NW * (q0 + (more ? sq : nr - 1u));
+        const uint32_t qi = q0 + (more ? sq : nr - 1u);
+        const uint32_t v = wv + NW * qi;
         const uint32_t jc = split == 1 ? v : v / split;  // the virtual run's chunk
-        issue(sg, b0, b1, jc, more);
+        issue(sg, b0, b1, jc, qi, more);
         if (more) {
           so = b1;
           if (so >= qe) {
@@ -741,6 +840,7 @@ __global__ __launch_bounds__(kBlk) void pb_tile_kernel(const uint8_t *__restrict
       }
     }
   }
+  flush_regs();
 }
 
 // ---------------------------------------------------------------- K6
@@ -877,8 +977,10 @@ int adl_bloom_probe_batch_device(const uint8_t *d_keys, const uint64_t *d_offset
   uint32_t *ent = reinterpret_cast<uint32_t *>(ws + p.o_ent);
   uint32_t *tab = reinterpret_cast<uint32_t *>(ws + p.o_tab);
   uint8_t *res = ws + p.o_res;
+  uint32_t *split = reinterpret_cast<uint32_t *>(ws + p.o_split);
   const uint32_t F = num_filters;
   const uint32_t cus = adl_host::device_cus();
+  const uint32_t g_tile = std::min(cus, kMaxSlots);  // pb_tile's workgroups
   const size_t lds_k1 = (size_t)(2 * F + 2) * 4;                       // counters + tile counts
   const size_t lds_k3 = (size_t)(2 * kQB + 5 * (F + 1) + 32) * 4;      // hashes + 5 per-filter arrays + scratch
   const size_t lds_k6 = (size_t)(kQB / 32 + 4 * (F + 1) + 32) * 4;     // answer bits + 4 per-filter arrays + scratch
@@ -898,7 +1000,8 @@ int adl_bloom_probe_batch_device(const uint8_t *d_keys, const uint64_t *d_offset
     uint32_t *gsum = reinterpret_cast<uint32_t *>(ws + p.o_gsum);
     hipLaunchKernelGGL(pb_colsum_kernel, dim3(p.ng), dim3(kBlk), 0, st, cnt, p.nb, F, gsum);
     ADL_HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(pb_plan_kernel, dim3(1), dim3(kBlk), 0, st, gsum, p.ng, F, p.C, p.maxch, desc, cf, scal);
+    hipLaunchKernelGGL(pb_plan_kernel, dim3(1), dim3(kBlk), 0, st, gsum, p.ng, F, p.C, p.maxch, desc, cf, scal, p.k,
+                       g_tile, split);
     ADL_HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(pb_starts_kernel, dim3(p.ng), dim3(kBlk), 0, st, cnt, gsum, p.nb, F, desc, start);
     ADL_HIP_TRY(hipGetLastError());
@@ -911,8 +1014,8 @@ int adl_bloom_probe_batch_device(const uint8_t *d_keys, const uint64_t *d_offset
       if (int rc = lim()) return rc;
       hipLaunchKernelGGL(kern, dim3(cus), dim3(kBlk), lds_p1, st, hs, desc, cf, scal, p.k, p.C, ent, tab, res, exp);
       ADL_HIP_TRY(hipGetLastError());
-      hipLaunchKernelGGL(pb_tile_kernel, dim3(cus), dim3(kBlk), lds_p2, st, d_bitmaps, desc, F, scal, p.k, p.C, ent,
-                         tab, res, exp);
+      hipLaunchKernelGGL(pb_tile_kernel, dim3(g_tile), dim3(kBlk), lds_p2, st, d_bitmaps, desc, F, scal, p.k, p.C,
+                         ent, tab, split, res, exp);
       ADL_HIP_TRY(hipGetLastError());
       return ADL_OK;
     };
