@@ -250,3 +250,24 @@ def test_probe_batch_shape_sweep(dev, ab, oracle, case):
     assert fid.size >= 1 << 20  # the binned path
     got = _check(dev, ab, oracle, arena, off, keys, fid, bpk=bpk)
     assert not got[fid >= F].any()
+
+
+# pb_tile's workgroups take contiguous tile ranges of about equal work
+# (pb_plan's split): a hot filter's tiles get a workgroup each and the
+# workgroups after them none; zero-byte filters between the hot and the cold
+# ones have no tiles.  The answers must not depend on that split.
+@pytest.mark.parametrize("hot_bytes,F", [(3 << 20, 64), (1 << 27, 5), (1 << 16, 600)])
+def test_probe_batch_hot_filter_split(dev, ab, oracle, hot_bytes, F):
+    rng = np.random.default_rng(hot_bytes + F)
+    sizes = np.full(F, max(7, hot_bytes // 8), np.int64)
+    sizes[0] = hot_bytes
+    sizes[1:4] = 0
+    off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.uint64)
+    arena = (rng.integers(0, 256, int(off[-1]) + 16, dtype=np.uint8) |
+             rng.integers(0, 256, int(off[-1]) + 16, dtype=np.uint8))
+    arena[-16:] = 0
+    n = (1 << 20) + 12345
+    fid = np.where(rng.random(n) < 0.9, 0, rng.integers(0, F + 1, n)).astype(np.uint32)
+    keys = rng.integers(0, 256, (n, 16), dtype=np.uint8)
+    got = _check(dev, ab, oracle, arena, off, keys, fid, bpk=10)
+    assert not got[fid >= F].any()
