@@ -28,7 +28,7 @@
 //
 // Designs measured slower (a direct atomicOr build, collapsed-key stamping,
 // live-key compaction, a bucketed pass A, split-seed hashing, dynamic tile
-// queues, ...) are not in this library; DESIGN.md §5 keeps their numbers and
+// queues, ...) are not in this library; HISTORY.md keeps their numbers and
 // git history their code.
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>

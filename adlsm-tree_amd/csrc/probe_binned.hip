@@ -422,7 +422,7 @@ __global__ __launch_bounds__(kBlk) void pb_scatter_kernel(const uint4 *__restric
 // are in flight into registers while the current one is sorted and stored.
 // All k bits of every query are binned in one round (the reference stops at
 // the first clear bit, src/filter_block.cpp:54-59; the answer is the AND
-// either way, and a two-round form measured slower: DESIGN.md §5).  KFIX = 0:
+// either way, and a two-round form measured slower: HISTORY.md).  KFIX = 0:
 // runtime k.
 template <int KFIX>
 __global__ __launch_bounds__(kBlk) void pb_bin_kernel(const uint2 *__restrict__ hs, const PFilter *__restrict__ desc,
