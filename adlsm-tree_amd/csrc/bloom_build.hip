@@ -71,7 +71,7 @@ constexpr uint32_t kHvKeys = 512;         // keys per hash_var_kernel run
 constexpr uint32_t kBlockA = 1024;        // pass A threads per workgroup (one workgroup per CU)
 constexpr uint32_t kDdLog2Max = 11;       // log2 slots of pass A's repeated-hash table, at most
 // LDS pass A leaves free on its CU (3 KiB): the resident probe server's
-// workgroup (probe_server.hip, 2 KiB) fits beside it, so a Get never waits for
+// workgroup (probe_server.hip, 2.25 KiB) fits beside it, so a Get never waits for
 // a build's persistent grid (DB::Get probes while DoCompaction builds,
 // src/db.cpp:164-172, 263).  The headline's chunk still fits 7 whole rounds.
 constexpr uint32_t kLdsReserveWords = 768;

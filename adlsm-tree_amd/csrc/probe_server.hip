@@ -11,16 +11,27 @@
 //   slot j (512 B)   queries (<= kMaxQ), k, per query the absolute device range
 //                    [begin, end) of its filter in the cache arena, key offsets
 //                    and key bytes; written by the host thread holding slot j
-//   bell[j] (u32)    request sequence number, written after the slot (release);
-//                    the 64 bells share 256 bytes, so one wave-wide load polls
-//                    every slot
+//   bell[j] (u32)    request sequence number (bit 31: the request is inline),
+//                    written after the request (release); the 64 bells share
+//                    256 bytes, so one wave-wide load polls every slot
+//   line[j] (64 B)   slots 0-3 only (the first four threads that probe): a
+//                    one-query request with a key of up to 40 bytes sits
+//                    here, beside its sequence number and a check word.  The
+//                    four lines are read in the same round trip as the bells
+//                    (one more 4-byte load per lane), so such a request costs
+//                    no second read across PCIe: single-key Gets 7.4-7.8 ->
+//                    6.4-6.6 us median (profiles/r05/r05srv_inline_ab.txt;
+//                    sixteen lines, four loads per lane, measured 9.0).  A
+//                    line read while the host was writing it fails its check
+//                    and is read again at the next poll
 //   done[j] (64 B)   word 0: the served sequence number (a restarted kernel's
 //                    starting point); word 1: the low 24 bits of that number
 //                    above the 8 answer bits.  Both in one 8-byte system-scope
 //                    store; the host takes its answers from word 1 alone
 //
-// The wave polls the bells, copies pending slots into LDS four at a time (one
-// load per lane per slot, one round trip for the group), hashes each query's
+// The wave polls the bells and the inline lines, copies pending slots into LDS
+// four at a time (one load per lane per slot, one round trip for the group;
+// an inline request is copied from the lines already in LDS), hashes each query's
 // key from LDS (hash_bytes), tests its k bits in the arena with eight loads in
 // flight at once, and writes the answers with the sequence numbers.  The host
 // thread spins on its done line.
@@ -35,7 +46,7 @@
 // the unanswered-for-50-us check is left for a kernel that failed (its
 // completion event reports the error: ADL_ERR_DEVICE).
 //
-// Footprint.  2 KiB of LDS and 32 VGPRs: the wave fits on a CU beside a
+// Footprint.  2.25 KiB of LDS and 32 VGPRs: the wave fits on a CU beside a
 // build's persistent pass-A workgroup, which leaves exactly that free, so a
 // Get is served while a compaction builds (reference: DB::Get probes filters
 // without a lock while DoCompaction runs, src/db.cpp:164-172, 263, 294).  The
@@ -65,6 +76,10 @@ constexpr uint32_t kSlots = 64;      // one per lane of the server wave
 constexpr uint32_t kSlotBytes = 512;
 constexpr uint32_t kGroup = 4;       // slots staged in LDS at a time (2 KiB)
 constexpr uint32_t kHdrBytes = 16;   // seq (unused by the device), n, k, key bytes
+constexpr uint32_t kInlineSlots = 4;       // slots whose one-query requests can sit in their bell line
+constexpr uint32_t kInlineKeyBytes = 40;
+constexpr uint32_t kInlineBit = 0x80000000u;  // in a bell: the request is in the slot's line
+constexpr uint32_t kLineCheck = 0x5EED5EEDu;  // the XOR of a line's 16 words
 constexpr uint32_t kRangeOff = kHdrBytes;                      // u64 begin, end per query
 constexpr uint32_t kKoffOff = kRangeOff + 16 * adl_srv::kMaxQ;  // u16 offsets, kMaxQ + 1
 constexpr uint32_t kKeyOff = kKoffOff + 2 * (adl_srv::kMaxQ + 8);
@@ -84,6 +99,19 @@ struct Done {
   uint32_t pad[14];
 };
 static_assert(sizeof(Done) == 64, "done line");
+
+// A one-query request inline in its slot's bell line: check = kLineCheck ^ the
+// XOR of the other 15 words, so a line torn between two requests (read while
+// the host wrote it) fails the check.
+struct Line {
+  uint32_t seq;    // the bell value of this request
+  uint32_t check;
+  uint32_t k_klen;  // k | key bytes << 8
+  uint32_t len;     // filter range bytes
+  uint64_t begin;   // filter range start (device address in the cache arena)
+  uint8_t key[kInlineKeyBytes];
+};
+static_assert(sizeof(Line) == 64, "line size");
 static_assert(adl_srv::kMaxQ == 8, "a done word holds 8 answer bits");
 
 struct Ctl {
@@ -98,6 +126,7 @@ struct Ctl {
 // lines, slots.
 struct Area {
   uint32_t bell[kSlots];
+  Line line[kInlineSlots];
   Ctl ctl;
   Done done[kSlots];
   Slot slot[kSlots];
@@ -109,17 +138,15 @@ __device__ __forceinline__ uint32_t ld_sys(const uint32_t *p) {
 
 __device__ __forceinline__ uint64_t now_ticks() { return __builtin_amdgcn_s_memrealtime(); }  // 100 MHz
 
-// Query q of a slot staged in LDS: 1 iff all k bits of its filter range are set.
-__device__ __forceinline__ uint32_t serve_query(const Slot &sl, uint32_t q) {
-  const uint32_t k = min(sl.k, 30u);
-  const uint64_t b0 = sl.range[2 * q], b1 = sl.range[2 * q + 1];
+// A query staged in LDS: 1 iff all k bits of its filter range [b0, b1) are set.
+__device__ __forceinline__ uint32_t serve_query(uint32_t k, uint64_t b0, uint64_t b1, const uint8_t *key,
+                                                uint32_t klen) {
+  k = min(k, 30u);
   // 0 for an empty range or a filter of 2^31 bits or more (src/filter_block.cpp:50)
   const uint32_t mbits = b1 > b0 && b1 - b0 <= 0x0fffffffull ? (uint32_t)((b1 - b0) * 8) : 0u;
   if (!mbits) return 0;
-  const uint32_t ko = min((uint32_t)sl.koff[q], adl_srv::kMaxKeyBytes);
-  const uint32_t ke = min(max((uint32_t)sl.koff[q + 1], ko), adl_srv::kMaxKeyBytes);
   uint32_t h1, h2;
-  hash_bytes(sl.keys + ko, ke - ko, kSeed1, kSeed2, h1, h2);
+  hash_bytes(key, klen, kSeed1, kSeed2, h1, h2);
   const FastMod mod = fastmod_for(mbits);
   const uint8_t *bm = reinterpret_cast<const uint8_t *>(b0);
   // the answer is the AND of the k bits (src/filter_block.cpp:54-59; the
@@ -138,15 +165,28 @@ __device__ __forceinline__ uint32_t serve_query(const Slot &sl, uint32_t q) {
   return all & 1u;
 }
 
+// Query q of a slot staged in LDS.
+__device__ __forceinline__ uint32_t serve_slot_query(const Slot &sl, uint32_t q) {
+  const uint32_t ko = min((uint32_t)sl.koff[q], adl_srv::kMaxKeyBytes);
+  const uint32_t ke = min(max((uint32_t)sl.koff[q + 1], ko), adl_srv::kMaxKeyBytes);
+  return serve_query(sl.k, sl.range[2 * q], sl.range[2 * q + 1], sl.keys + ko, ke - ko);
+}
+
+// The request of a line staged in LDS.
+__device__ __forceinline__ uint32_t serve_line(const Line &ln) {
+  return serve_query(ln.k_klen & 0xFFu, ln.begin, ln.begin + ln.len, ln.key, min(ln.k_klen >> 8, kInlineKeyBytes));
+}
+
 // One wave.  Lane l polls bell l.  Pending slots are staged kGroup at a time
 // in 2 KiB of LDS (one 8-byte load per lane per slot, all in flight at once);
 // lane 8u + q then answers query q of the group's slot u.  The small footprint
-// (2 KiB of LDS, 32 VGPRs) lets the wave run beside a build's persistent
+// (2.25 KiB of LDS, 32 VGPRs) lets the wave run beside a build's persistent
 // workgroups, which leave exactly that much of their CU free (bloom_build.hip,
 // kLdsReserveWords): a Get does not wait for a build.
 __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(16))) void probe_server_kernel(
     Area *area, uint64_t idle_ticks, uint64_t life_ticks, uint32_t gen) {
   __shared__ __attribute__((aligned(16))) uint8_t lslot[kGroup][kSlotBytes];
+  __shared__ __attribute__((aligned(16))) uint32_t lline[kInlineSlots * 16];  // the lines of the last poll
   const uint32_t lane = threadIdx.x;
   // a successor queued behind a running kernel (Server::launcher) announces
   // itself: alive again, and its generation started
@@ -162,10 +202,27 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(16))) void probe
   for (;;) {
     const uint64_t tp = now_ticks();  // this poll (diagnostics: the gap since the previous one)
     const uint32_t bell = ld_sys(&area->bell[lane]);
-    const bool pend = bell != served;
+    // the inline lines, in the same round trip: lane l reads word l % 16 of
+    // line l / 16
+    const uint32_t lw = ld_sys(reinterpret_cast<const uint32_t *>(area->line) + lane);
+    bool pend = bell != served;
+    const bool rung = __ballot(pend) != 0;  // (before the line checks)
+    if (__ballot(pend && (bell & kInlineBit)) != 0) {
+      // some request is inline: the lines into LDS; line i is checked across
+      // lanes 16i .. 16i + 15 and judged by lane i
+      lline[lane] = lw;
+      uint32_t x = lw;
+#pragma unroll
+      for (uint32_t o = 1; o < 16; o <<= 1) x ^= (uint32_t)__shfl_xor((int)x, (int)o);
+      const uint32_t xi = (uint32_t)__shfl((int)x, (int)(16 * (lane & (kInlineSlots - 1))));
+      const uint32_t si = (uint32_t)__shfl((int)lw, (int)(16 * (lane & (kInlineSlots - 1))));
+      __syncthreads();
+      if (pend && (bell & kInlineBit)) pend = lane < kInlineSlots && si == bell && xi == kLineCheck;
+      // (a torn or stale line is read again at the next poll)
+    }
     const uint64_t pm = __ballot(pend);
     if (pm == 0) {
-      if (closing) break;
+      if (closing && !rung) break;  // (a torn line of the last poll is read again)
       const uint64_t t = tp;
       tprev = tp;
       const bool stop = __ballot(ld_sys(&area->ctl.stop[lane & 15]) != 0) != 0;
@@ -191,8 +248,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(16))) void probe
       for (uint32_t u = 0; u < kGroup; ++u) {
         js[u] = m ? (uint32_t)__builtin_ctzll(m) : kSlots;
         m &= m - 1;  // (m = 0 stays 0)
+        // (an inline request's slot is not read: its line is in LDS)
+        const uint32_t bj = (uint32_t)__shfl((int)bell, (int)(js[u] < kSlots ? js[u] : 0u));
         const uint64_t *src = reinterpret_cast<const uint64_t *>(&area->slot[js[u] < kSlots ? js[u] : 0]);
-        v[u] = __hip_atomic_load(src + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        v[u] = js[u] < kSlots && !(bj & kInlineBit) ? __hip_atomic_load(src + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+                                                     : 0ull;
       }
 #pragma unroll
       for (uint32_t u = 0; u < kGroup; ++u) reinterpret_cast<uint64_t *>(lslot[u])[lane] = v[u];
@@ -202,9 +262,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(16))) void probe
 #pragma unroll
       for (uint32_t x = 0; x < kGroup; ++x) j = u == x ? js[x] : j;
       uint32_t hit = 0;
-      if (j < kSlots) {
+      const uint32_t bj = (uint32_t)__shfl((int)bell, (int)(j < kSlots ? j : 0u));
+      if (j < kSlots && (bj & kInlineBit)) {
+        if (q == 0) hit = serve_line(*reinterpret_cast<const Line *>(&lline[16 * (j & (kInlineSlots - 1))]));
+      } else if (j < kSlots) {
         const Slot &sl = *reinterpret_cast<const Slot *>(lslot[u]);
-        if (q < min(sl.n, adl_srv::kMaxQ)) hit = serve_query(sl, q);
+        if (q < min(sl.n, adl_srv::kMaxQ)) hit = serve_slot_query(sl, q);
       }
       const uint64_t hb = __ballot(hit != 0);
       // lane u < kGroup answers slot js[u]: {seq, (seq << 8) | answer bits} in
@@ -513,18 +576,41 @@ int probe(Server *s, const uint8_t *h_keys, const uint64_t *h_offsets, uint32_t 
     my_server = s->id;
   }
   std::lock_guard<std::mutex> slot_guard(s->slot_mu[my]);
-  Slot &sl = s->host->slot[my];
-  sl.n = (uint32_t)n;
-  sl.k = k;
-  sl.key_bytes = (uint32_t)key_bytes;
-  for (uint64_t q = 0; q < n; ++q) {
-    sl.range[2 * q] = range[2 * q];
-    sl.range[2 * q + 1] = range[2 * q + 1];
-    sl.koff[q] = (uint16_t)(h_offsets ? h_offsets[q] - h_offsets[0] : q * key_stride);
+  // 31-bit sequence numbers, never 0 (the initial done); bit 31 of the bell
+  // value says where the request is
+  s->seq[my] = (s->seq[my] + 1) & ~kInlineBit;
+  if (s->seq[my] == 0) s->seq[my] = 1;
+  const bool inl = my < kInlineSlots && n == 1 && key_bytes <= kInlineKeyBytes && range[1] >= range[0] &&
+                   range[1] - range[0] <= 0xFFFFFFFFull && k < 256;
+  const uint32_t seq = s->seq[my] | (inl ? kInlineBit : 0u);
+  const uint8_t *kp = h_keys + (h_offsets ? h_offsets[0] : 0);
+  if (inl) {
+    // the whole line, check word last computed, in one copy; then the bell
+    Line ln{};
+    ln.seq = seq;
+    ln.k_klen = k | (uint32_t)key_bytes << 8;
+    ln.len = (uint32_t)(range[1] - range[0]);
+    ln.begin = range[0];
+    memcpy(ln.key, kp, key_bytes);
+    uint32_t w[16];
+    memcpy(w, &ln, sizeof(ln));
+    uint32_t x = kLineCheck;
+    for (uint32_t i = 0; i < 16; ++i) x ^= i == 1 ? 0u : w[i];
+    ln.check = x;
+    memcpy(&s->host->line[my], &ln, sizeof(ln));
+  } else {
+    Slot &sl = s->host->slot[my];
+    sl.n = (uint32_t)n;
+    sl.k = k;
+    sl.key_bytes = (uint32_t)key_bytes;
+    for (uint64_t q = 0; q < n; ++q) {
+      sl.range[2 * q] = range[2 * q];
+      sl.range[2 * q + 1] = range[2 * q + 1];
+      sl.koff[q] = (uint16_t)(h_offsets ? h_offsets[q] - h_offsets[0] : q * key_stride);
+    }
+    sl.koff[n] = (uint16_t)key_bytes;
+    memcpy(sl.keys, kp, key_bytes);
   }
-  sl.koff[n] = (uint16_t)key_bytes;
-  memcpy(sl.keys, h_keys + (h_offsets ? h_offsets[0] : 0), key_bytes);
-  const uint32_t seq = ++s->seq[my] == 0 ? ++s->seq[my] : s->seq[my];  // never 0 (the initial done)
   // bell, then alive, both sequentially consistent (the kernel clears alive
   // and then polls once more: probe_server_kernel)
   __atomic_store_n(&s->host->bell[my], seq, __ATOMIC_SEQ_CST);
