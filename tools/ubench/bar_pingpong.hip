@@ -8,7 +8,9 @@
 // that the host writes through the BAR, so the wave polls local memory and
 // only the host's posted writes and the answer cross the bus.
 //
-// usage: bar_pingpong host|fine|uncached|nopayload|wide [calls]
+// usage: bar_pingpong host|fine|uncached|nopayload|wide|pipe2|pipe4 [calls]
+//   pipe2 / pipe4: host memory, no request read, the wave keeps 2 / 4 bell
+//         polls in flight (a new one issued as the oldest returns)
 //   nopayload: host memory, the wave answers without reading the request
 //   wide: host memory, the wave polls 64 bell lines of 64 B (4 KiB) per poll,
 //         as if each request sat inline in its bell line (one round trip)
@@ -64,11 +66,35 @@ __global__ void pingpong(const uint32_t *bell, const uint64_t *req, uint32_t *an
   }
 }
 
+// bell polls kept D deep: each iteration waits for the oldest poll only
+template <int D>
+__global__ void pingpong_pipe(const uint32_t *bell, uint32_t *ans, uint32_t n, uint64_t timeout_ticks) {
+  const int lane = threadIdx.x;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  uint32_t b[D];
+#pragma unroll
+  for (int d = 0; d < D; ++d) b[d] = __hip_atomic_load(bell, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  uint32_t i = 1;
+  while (i <= n) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      const uint32_t v = __shfl(b[d], 0);
+      b[d] = __hip_atomic_load(bell, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (v == i) {
+        if (lane == 0) __hip_atomic_store(ans, i, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        ++i;
+      }
+    }
+    if (__builtin_amdgcn_s_memrealtime() - t0 > timeout_ticks) return;
+  }
+}
+
 int main(int argc, char **argv) {
   const char *mode = argc > 1 ? argv[1] : "host";
   const uint32_t n = argc > 2 ? (uint32_t)atoi(argv[2]) : 20000;
   void *area = nullptr;  // bell (word 0) + request (from byte 256)
-  const bool nopayload = !strcmp(mode, "nopayload"), wide = !strcmp(mode, "wide");
+  const int pipe = !strcmp(mode, "pipe2") ? 2 : !strcmp(mode, "pipe4") ? 4 : 0;
+  const bool nopayload = !strcmp(mode, "nopayload") || pipe, wide = !strcmp(mode, "wide");
   if (!strcmp(mode, "host") || nopayload || wide) {
     CHECK(hipHostMalloc(&area, 8192, hipHostMallocCoherent | hipHostMallocMapped));
   } else if (!strcmp(mode, "fine")) {
@@ -105,8 +131,13 @@ int main(int argc, char **argv) {
   const uint64_t *dreq = reinterpret_cast<const uint64_t *>((const uint8_t *)area + 256);
   hipStream_t st;
   CHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
-  hipLaunchKernelGGL(pingpong, dim3(1), dim3(64), 0, st, dbell, wide || nopayload ? nullptr : dreq, ans, n,
-                     (uint64_t)100000000 * 5, (int)wide);  // 5 s
+  if (pipe == 2)
+    hipLaunchKernelGGL(pingpong_pipe<2>, dim3(1), dim3(64), 0, st, dbell, ans, n, (uint64_t)100000000 * 5);
+  else if (pipe == 4)
+    hipLaunchKernelGGL(pingpong_pipe<4>, dim3(1), dim3(64), 0, st, dbell, ans, n, (uint64_t)100000000 * 5);
+  else
+    hipLaunchKernelGGL(pingpong, dim3(1), dim3(64), 0, st, dbell, wide || nopayload ? nullptr : dreq, ans, n,
+                       (uint64_t)100000000 * 5, (int)wide);  // 5 s
   CHECK(hipGetLastError());
   std::vector<double> us;
   us.reserve(n);
