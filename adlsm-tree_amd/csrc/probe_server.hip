@@ -619,10 +619,18 @@ int probe(Server *s, const uint8_t *h_keys, const uint64_t *h_offsets, uint32_t 
   const auto tb = std::chrono::steady_clock::now();
   bool relaunched = false;
   if (!__atomic_load_n(&s->host->ctl.alive, __ATOMIC_SEQ_CST)) {
-    std::lock_guard<std::mutex> g(s->launch_mu);
-    const uint32_t gen0 = s->gen;
-    if (int rc = ensure_running(s, my, seq, &bits, &done)) return rc;
-    relaunched = s->gen != gen0;
+    // Only if no one else is launching: the holder of launch_mu is the
+    // launcher thread queueing a successor (or a thread relaunching), whose
+    // kernel polls every bell.  Waiting for the lock made a Get at a hand-over
+    // wait out a stalled launch call (one of 50 000 idle Gets took 709 us,
+    // profiles/r05/r05f2_coexist.json); a request still unanswered after 50 us
+    // takes the lock below in any case.
+    std::unique_lock<std::mutex> g(s->launch_mu, std::try_to_lock);
+    if (g.owns_lock()) {
+      const uint32_t gen0 = s->gen;
+      if (int rc = ensure_running(s, my, seq, &bits, &done)) return rc;
+      relaunched = s->gen != gen0;
+    }
   }
   const auto t0 = std::chrono::steady_clock::now();
   auto since = [&] { return std::chrono::steady_clock::now() - t0; };
