@@ -553,7 +553,8 @@ __global__ __launch_bounds__(kBlk) void pb_bin_kernel(const uint2 *__restrict__ 
 }
 
 // ---------------------------------------------------------------- P2
-// Persistent over the tiles (XCD-consecutive order).  The next tile's bitmap
+// Persistent: each workgroup takes a contiguous range of tiles of about equal
+// work (pb_plan's split; consecutive ranges on one XCD).  The next tile's bitmap
 // bytes are in flight into registers while the current tile's runs are
 // tested; each wave stages the (start, end) of all its chunks' runs in two
 // registers at the tile's start and keeps two runs' loads in flight.
@@ -589,9 +590,8 @@ __device__ __forceinline__ TileRef tile_ref(const PFilter *desc, const uint32_t 
 }
 
 __global__ __launch_bounds__(kBlk) void pb_tile_kernel(const uint8_t *__restrict__ bitmaps,
-                                                       const PFilter *__restrict__ desc, uint32_t F,
-                                                       const uint32_t *__restrict__ scal, uint32_t k, uint32_t C,
-                                                       const uint32_t *__restrict__ ent,
+                                                       const PFilter *__restrict__ desc, uint32_t F, uint32_t k,
+                                                       uint32_t C, const uint32_t *__restrict__ ent,
                                                        const uint32_t *__restrict__ table,
                                                        const uint32_t *__restrict__ split,
                                                        uint8_t *__restrict__ res, uint32_t exp) {
@@ -1014,8 +1014,8 @@ int adl_bloom_probe_batch_device(const uint8_t *d_keys, const uint64_t *d_offset
       if (int rc = lim()) return rc;
       hipLaunchKernelGGL(kern, dim3(cus), dim3(kBlk), lds_p1, st, hs, desc, cf, scal, p.k, p.C, ent, tab, res, exp);
       ADL_HIP_TRY(hipGetLastError());
-      hipLaunchKernelGGL(pb_tile_kernel, dim3(g_tile), dim3(kBlk), lds_p2, st, d_bitmaps, desc, F, scal, p.k, p.C,
-                         ent, tab, split, res, exp);
+      hipLaunchKernelGGL(pb_tile_kernel, dim3(g_tile), dim3(kBlk), lds_p2, st, d_bitmaps, desc, F, p.k, p.C, ent, tab,
+                         split, res, exp);
       ADL_HIP_TRY(hipGetLastError());
       return ADL_OK;
     };
