@@ -1,7 +1,7 @@
 set -u
 cd "$(dirname "$0")/.."
 OUT=gpurun_out/srv_inline; mkdir -p $OUT
-timeout -k 10 400 python -u -m pytest tests/test_gpu_readpath.py -q -x --timeout 200 --timeout-method thread -p no:cacheprovider > $OUT/pytest_readpath.log 2>&1
+timeout -k 10 150 python -u -m pytest tests/test_gpu_readpath.py -q -x --timeout 60 --timeout-method thread -p no:cacheprovider > $OUT/pytest_readpath.log 2>&1
 rc=$?; tail -3 $OUT/pytest_readpath.log; [ $rc -ne 0 ] && exit $rc
 for rep in 1 2; do
   for v in base new; do
