@@ -117,6 +117,7 @@ def lib() -> ctypes.CDLL:
         "adl_bloom_get_device": (ctypes.c_int, [ctypes.POINTER(i32)]),
         "adl_bloom_set_device": (ctypes.c_int, [i32]),
         "adl_bloom_reload_knobs": (ctypes.c_int, []),
+        "adl_bloom_probe_server_launches": (ctypes.c_int, [ctypes.POINTER(u64)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -409,6 +410,13 @@ TEST_FAULT_CACHE_COMPLETION = 2
 def test_fault(site: int, arg: int) -> None:
     """Arm (arg >= 0) or disarm (arg < 0) a one-shot injected failure."""
     _check(lib().adl_bloom_test_fault(site, arg), "adl_bloom_test_fault")
+
+
+def probe_server_launches() -> int:
+    """Probe-server kernels this process has launched (relaunches included)."""
+    n = ctypes.c_uint64(0)
+    _check(lib().adl_bloom_probe_server_launches(ctypes.byref(n)), "adl_bloom_probe_server_launches")
+    return n.value
 
 
 def profile_enable(capacity: int = 4096) -> None:

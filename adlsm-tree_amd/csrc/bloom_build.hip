@@ -1570,12 +1570,17 @@ int launch_binned_dt(const Plan &p, Keys keys, uint8_t *d_bitmaps, void *ws, hip
   uint32_t *tab_ws = pos_ws + p.pos_words;
   uint32_t *scr = tab_ws + p.table_words;  // the work-queue counters, pass A's per-wave scratch lines
   uint2 *hp = reinterpret_cast<uint2 *>(scr + p.scratch_words);
-  // While a resident probe server exists (a reader process), the passes take
-  // their chunks / tiles from the work queues: a workgroup slowed or held back
-  // by the server's wave on its CU then takes less work instead of holding up
-  // the pass (reads beside builds).  The counters start at 0.
-  const bool live = adl_srv::live_servers() > 0;
-  const bool dyn_a = live && p.grid_a % 8 == 0, dyn_b = live && p.grid_b % 8 == 0;
+  // While a probe server's kernel is resident (Gets are being served), the
+  // passes take their chunks / tiles from the work queues: a workgroup slowed
+  // or held back by the server's wave on its CU then takes less work instead
+  // of holding up the pass (reads beside builds).  The counters
+  // start at 0.  (Round 5 switched whenever a server object existed, so every
+  // build of a process that had served one Get paid the queues' cost.)
+  const adl_host::Knobs &kn = adl_host::knobs();
+  const bool live = kn.build_queues == 3 || (kn.build_queues == 1 && adl_srv::live_servers() > 0) ||
+                    (kn.build_queues == 2 && adl_srv::resident_servers() > 0);
+  const bool dyn_a = live && (kn.build_queue_passes & 1) && p.grid_a % 8 == 0;
+  const bool dyn_b = live && (kn.build_queue_passes & 2) && p.grid_b % 8 == 0;
   if (dyn_a || dyn_b) ADL_HIP_TRY(hipMemsetAsync(scr, 0, kQueueWords * 4, st));
   FilterTable ft{};
   if constexpr (DT) {

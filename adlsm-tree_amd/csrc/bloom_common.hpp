@@ -202,6 +202,12 @@ struct Knobs {
   uint64_t server_idle_us = 2000;   // ADL_BLOOM_SERVER_IDLE_US
   uint64_t server_life_us = 1000000;  // ADL_BLOOM_SERVER_LIFE_US
   uint64_t pipe_mb = 128;         // ADL_BLOOM_PIPE_MB: keys per group of the pipelined host build
+  // ADL_BLOOM_BUILD_QUEUES: when the build passes take their items from work
+  // queues instead of the static order: 0 never, 1 while a probe server
+  // exists, 2 while a server kernel is resident (its alive word), 3 always.
+  // ADL_BLOOM_BUILD_QUEUE_PASSES: which passes (bit 0 pass A, bit 1 pass B).
+  uint32_t build_queues = 2;
+  uint32_t build_queue_passes = 3;
   bool debug = false;             // ADL_BLOOM_DEBUG: the plan and failing HIP calls to stderr
   uint32_t exp = 0, pb_exp = 0;   // ADL_BLOOM_EXP / ADL_PB_EXP: diagnostics build (make stamps) only
 
@@ -220,6 +226,8 @@ struct Knobs {
     server_idle_us = u64("ADL_BLOOM_SERVER_IDLE_US", 2000);
     server_life_us = u64("ADL_BLOOM_SERVER_LIFE_US", 1000000);
     pipe_mb = u64("ADL_BLOOM_PIPE_MB", 128);
+    build_queues = (uint32_t)u64("ADL_BLOOM_BUILD_QUEUES", 2);
+    build_queue_passes = (uint32_t)u64("ADL_BLOOM_BUILD_QUEUE_PASSES", 3);
     debug = u64("ADL_BLOOM_DEBUG", 0) != 0;
 #ifdef ADL_BLOOM_STAMPS
     exp = (uint32_t)u64("ADL_BLOOM_EXP", 0);
@@ -435,7 +443,7 @@ int lds_limit() {
 __attribute__((visibility("hidden"))) int adl_probe_ranges_device_ev(
     const uint8_t *d_keys, const uint64_t *d_offsets, uint64_t n, uint32_t key_stride, const uint32_t *d_filter_id,
     uint32_t num_filters, const uint8_t *d_bitmaps, const uint64_t *d_begin, const uint64_t *d_end,
-    int32_t bits_per_key, uint8_t *d_out, hipStream_t st, hipEvent_t done);
+    const uint8_t *d_k, uint8_t *d_out, hipStream_t st, hipEvent_t done);
 
 // adl_bloom_test_fault's armed sites (-1: off).  take() disarms and returns the
 // argument, so an armed fault fires once.

@@ -55,17 +55,19 @@ __global__ __launch_bounds__(kBlockP) void bloom_probe_kernel(Keys keys, uint64_
 }
 
 // Multi-filter probe: query i against filter fid[i] (or uniform_f).  Each
-// filter has its own divisor m = 8 * bitmap bytes; the magic-multiply
-// constants of up to kLdsFilters filters are built once per workgroup into
-// LDS (dynamic, 8 B per filter), beyond that per query.
+// filter has its own divisor m = 8 * bitmap bytes, and -- when kf is given --
+// its own probe count kf[f] (blocks written with different bits_per_key: the
+// reference reads bpk per block, src/filter_block.cpp:158-170).  The
+// magic-multiply constants and k of up to kLdsFilters filters are built once
+// per workgroup into LDS (dynamic, 8 B per filter), beyond that per query.
 struct ModLds {
-  uint32_t magic, shift;
+  uint32_t magic, shift_k;  // shift | k << 8
 };
 
 template <class Keys>
 __global__ __launch_bounds__(kBlockP) void bloom_probe_multi_kernel(
-    Keys keys, uint64_t n, uint32_t k, const uint32_t *__restrict__ fid, uint32_t uniform_f,
-    uint32_t nf, const uint8_t *__restrict__ bitmaps, const uint64_t *__restrict__ boff,
+    Keys keys, uint64_t n, uint32_t k, const uint8_t *__restrict__ kf, const uint32_t *__restrict__ fid,
+    uint32_t uniform_f, uint32_t nf, const uint8_t *__restrict__ bitmaps, const uint64_t *__restrict__ boff,
     const uint64_t *__restrict__ bend, uint8_t *__restrict__ out) {
   // filter f = bitmaps[boff[f], bend[f]), or [boff[f], boff[f+1]) when bend is null
   extern __shared__ ModLds lmod[];
@@ -77,7 +79,7 @@ __global__ __launch_bounds__(kBlockP) void bloom_probe_multi_kernel(
       const uint64_t bytes = (bend ? bend[f] : boff[f + 1]) - boff[f];
       const uint32_t m = bytes <= 0x0fffffffull ? (uint32_t)(bytes * 8) : 0u;
       const FastMod fm = m ? fastmod_for(m) : FastMod{};
-      lmod[f] = ModLds{fm.magic, fm.shift};
+      lmod[f] = ModLds{fm.magic, fm.shift | (kf ? (uint32_t)kf[f] : k) << 8};
     }
     __syncthreads();
   }
@@ -92,15 +94,18 @@ __global__ __launch_bounds__(kBlockP) void bloom_probe_multi_kernel(
       const uint32_t m = b1 - b0 <= 0x0fffffffull ? (uint32_t)((b1 - b0) * 8) : 0u;
       if (m != 0) {
         FastMod mod;
+        uint32_t kq;
         if (lds_tab) {
           const ModLds e = lmod[f];
-          mod = FastMod{m, e.magic, e.shift, 0u};
+          mod = FastMod{m, e.magic, e.shift_k & 0xFFu, 0u};
+          kq = e.shift_k >> 8;
         } else {
           mod = fastmod_for(m);
+          kq = kf ? (uint32_t)kf[f] : k;
         }
         uint32_t h1, h2;
         keys.hash(i, h1, h2);
-        hit = probe_bits(bitmaps + b0, h1, h2, k, mod);
+        hit = probe_bits(bitmaps + b0, h1, h2, kq, mod);
       }
     }
     out[i] = hit;
@@ -267,7 +272,7 @@ int probe_multi(const uint8_t *d_keys, const uint64_t *d_offsets, uint64_t n, ui
                 const uint32_t *d_filter_id, uint32_t uniform_f, uint32_t num_filters,
                 const uint8_t *d_bitmaps, const uint64_t *d_bitmap_off, int32_t bits_per_key,
                 uint8_t *d_out, hipStream_t st, const uint64_t *d_bitmap_end = nullptr,
-                hipEvent_t done = nullptr) {
+                hipEvent_t done = nullptr, const uint8_t *d_k = nullptr) {
   if (num_filters && (!d_bitmaps || !d_bitmap_off)) return ADL_ERR_INVALID_ARG;
   if (!d_offsets && key_stride == 0) return ADL_ERR_INVALID_ARG;
   const uint32_t k = (uint32_t)adl_host::num_probes(bits_per_key);
@@ -275,7 +280,7 @@ int probe_multi(const uint8_t *d_keys, const uint64_t *d_offsets, uint64_t n, ui
     const size_t lds = num_filters <= kLdsFilters ? (size_t)num_filters * sizeof(ModLds) : 0;
     // `done` rides on the dispatch packet itself (no marker packet after it)
     hipExtLaunchKernelGGL(bloom_probe_multi_kernel<decltype(keys)>, dim3(grid_for(n, kBlockP, 8)),
-                          dim3(kBlockP), lds, st, nullptr, done, 0, keys, n, k, d_filter_id,
+                          dim3(kBlockP), lds, st, nullptr, done, 0, keys, n, k, d_k, d_filter_id,
                           uniform_f, num_filters, d_bitmaps, d_bitmap_off, d_bitmap_end, d_out);
     ADL_HIP_TRY(hipGetLastError());
     return ADL_OK;
@@ -283,17 +288,18 @@ int probe_multi(const uint8_t *d_keys, const uint64_t *d_offsets, uint64_t n, ui
 }
 }  // namespace
 
-// adl_bloom_probe_ranges_device whose launch also completes `done` (the
-// filter cache's small batches wait on it; see filter_cache.hip).
+// adl_bloom_probe_ranges_device with a probe count per filter (d_k[f]), whose
+// launch also completes `done` (the filter cache's small batches wait on it;
+// see filter_cache.hip).
 int adl_host::adl_probe_ranges_device_ev(const uint8_t *d_keys, const uint64_t *d_offsets, uint64_t n, uint32_t key_stride,
                                const uint32_t *d_filter_id, uint32_t num_filters, const uint8_t *d_bitmaps,
-                               const uint64_t *d_begin, const uint64_t *d_end, int32_t bits_per_key, uint8_t *d_out,
+                               const uint64_t *d_begin, const uint64_t *d_end, const uint8_t *d_k, uint8_t *d_out,
                                hipStream_t st, hipEvent_t done) {
   if (n == 0) return ADL_OK;
-  if (!d_keys || !d_filter_id || !d_out || bits_per_key < 0) return ADL_ERR_INVALID_ARG;
+  if (!d_keys || !d_filter_id || !d_out || (num_filters && !d_k)) return ADL_ERR_INVALID_ARG;
   if (num_filters && !d_end) return ADL_ERR_INVALID_ARG;
-  return probe_multi(d_keys, d_offsets, n, key_stride, d_filter_id, 0, num_filters, d_bitmaps, d_begin,
-                     bits_per_key, d_out, st, d_end, done);
+  return probe_multi(d_keys, d_offsets, n, key_stride, d_filter_id, 0, num_filters, d_bitmaps, d_begin, 10, d_out,
+                     st, d_end, done, d_k);
 }
 
 extern "C" int adl_bloom_probe_ranges_device(const uint8_t *d_keys, const uint64_t *d_offsets, uint64_t n,

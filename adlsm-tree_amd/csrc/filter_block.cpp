@@ -293,15 +293,17 @@ RC FilterCache::Probe(const vector<string_view> &oids, const vector<uint32_t> &t
   return FromStatus(st);
 }
 
-FilterCache *FilterCache::Shared(int bits_per_key) {
+FilterCache *FilterCache::Shared(int) { return Shared(); }
+
+FilterCache *FilterCache::Shared() {
   struct Slot {
     FilterCache *cache = nullptr;
     std::chrono::steady_clock::time_point retry_after{};  // after a failed creation
   };
   static std::mutex mu;
-  static std::map<int, Slot> *caches = new std::map<int, Slot>;  // kept until exit
+  static Slot *slot = new Slot;  // kept until exit
   std::lock_guard<std::mutex> g(mu);
-  Slot &s = (*caches)[bits_per_key];
+  Slot &s = *slot;
   if (s.cache) return s.cache;  // only created (OK) caches are stored
   // A failed creation is not retried on every reader open (each try holds this
   // lock over up to three arena allocations): not again for a second.
@@ -313,7 +315,7 @@ FilterCache *FilterCache::Shared(int bits_per_key) {
   // the GPU): a quarter, then a sixteenth; a size the user set is taken as is
   const int tries = e ? 1 : 3;
   for (int i = 0; i < tries; ++i, bytes /= 4) {
-    FilterCache *c = new FilterCache(bytes, 1u << 20, bits_per_key);
+    FilterCache *c = new FilterCache(bytes, 1u << 20);
     if (c->status() == OK) {
       s.cache = c;
       return c;
@@ -359,7 +361,7 @@ RC FilterBlockReader::Parse(string_view filter_blocks) {
 
 RC FilterBlockReader::Init(string_view filter_blocks) {
   if (RC rc = Parse(filter_blocks); rc) return rc;
-  FilterCache *c = FilterCache::Shared(bits_per_key_);
+  FilterCache *c = FilterCache::Shared();
   if (!c) return Upload();  // no shared arena: a device copy of its own
   static std::atomic<uint64_t> next_id{0};
   oid_ = "\x01reader:" + std::to_string(next_id.fetch_add(1));
@@ -376,7 +378,8 @@ RC FilterBlockReader::Init(string_view filter_blocks) {
 
 RC FilterBlockReader::Init(string_view filter_blocks, FilterCache &cache, string_view oid) {
   if (RC rc = Parse(filter_blocks); rc) return rc;
-  if (cache.bits_per_key() != bits_per_key_) return FILTER_BLOCK_ERROR;
+  // (the cache keeps this block's own bits_per_key with its entry: tables of
+  // any bpk share one cache, as Level::Get reads them, src/revision.cpp:265-310)
   oid_.assign(oid.data(), oid.size());
   cache_ = &cache;
   own_oid_ = false;

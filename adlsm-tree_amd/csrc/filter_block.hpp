@@ -150,7 +150,9 @@ class FilterBlockWriter {
  * thread-safe, and no lock is held while a probe runs on the device. */
 class FilterCache {
  public:
-  FilterCache(uint64_t capacity_bytes, uint32_t max_tables, int bits_per_key);
+  /* bits_per_key: kept for source compatibility; blocks of any bits_per_key
+   * are accepted, each probed with the k of its own "bf:" info */
+  FilterCache(uint64_t capacity_bytes, uint32_t max_tables, int bits_per_key = 10);
   ~FilterCache();
   FilterCache(const FilterCache &) = delete;
   FilterCache &operator=(const FilterCache &) = delete;
@@ -166,8 +168,10 @@ class FilterCache {
   RC Probe(const vector<string_view> &oids, const vector<uint32_t> &table, const KeyArena &keys, int filter,
            vector<uint8_t> &out, uint64_t *uncached = nullptr);
   /* The process-wide cache FilterBlockReader::Init(string_view) keeps its
-   * bitmaps in, one per bits_per_key (arena ADL_BLOOM_READER_CACHE_BYTES,
-   * default 1 GiB); created on first use and kept until exit. */
+   * bitmaps in, for blocks of every bits_per_key (arena
+   * ADL_BLOOM_READER_CACHE_BYTES, default 1 GiB); created on first use and
+   * kept until exit.  (Shared(int) is the round-5 spelling: the same cache.) */
+  static FilterCache *Shared();
   static FilterCache *Shared(int bits_per_key);
 
  private:
@@ -186,7 +190,7 @@ class FilterBlockReader {
   ~FilterBlockReader();
   FilterBlockReader(const FilterBlockReader &) = delete;
   FilterBlockReader &operator=(const FilterBlockReader &) = delete;
-  /* src/filter_block.hpp:57: the bitmaps go into FilterCache::Shared(bpk)
+  /* src/filter_block.hpp:57: the bitmaps go into FilterCache::Shared()
    * under an id private to this reader (removed by the destructor) */
   RC Init(string_view filter_block);
   /* the same, with the table's entry in `cache` under `oid`: every reader of

@@ -33,6 +33,7 @@
 //    no lock for the duration of a lookup.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <chrono>
 #include <stdint.h>
 #include <string.h>
@@ -53,15 +54,20 @@ namespace {
 
 constexpr uint64_t kAlign = 256;
 constexpr uint64_t kOnesBytes = 16;  // an all-ones 16-byte filter: every probe hits
+constexpr int64_t kServerBackoffNs = 1000000000;  // launched probes for 1 s after a starved server request
 
 // FilterBlockReader::Init's trailer walk (src/filter_block.cpp:113-155, in
 // filter_block_format.hpp): bitmaps region [0, offsets_start), filter f =
-// [off_f, off_{f+1} or offsets_start); one bits_per_key (so one k) per cache.
-int parse_block(const uint8_t *b, uint64_t len, int32_t want_bpk, std::vector<uint64_t> &off) {
+// [off_f, off_{f+1} or offsets_start).  Each block carries its own
+// bits_per_key in its "bf:" info, and the reference builds its BloomFilter
+// from it per block (CreateFilterAlgorithm, src/filter_block.cpp:158-170),
+// so a level may mix tables written under different DBOptions::bits_per_key
+// (src/options.hpp:24): the block's k is kept with its entry.
+int parse_block(const uint8_t *b, uint64_t len, std::vector<uint64_t> &off, uint8_t &k) {
   adl_fmt::FilterBlockLayout lay;
   if (adl_fmt::parse_filter_block(b, len, lay)) return ADL_FILTER_BLOCK_ERROR;
-  if (lay.bits_per_key != want_bpk) return ADL_ERR_INVALID_ARG;
   off = std::move(lay.off);
+  k = (uint8_t)adl_host::num_probes(lay.bits_per_key);
   return ADL_OK;
 }
 
@@ -91,6 +97,7 @@ struct adl_bloom_filter_cache {
     std::string oid;
     uint64_t base = 0, size = 0;  // arena range [base, base + size)
     std::vector<uint64_t> off;    // block-relative filter offsets (F+1)
+    uint8_t k = 1;                // probes per key: from the block's own bits_per_key
     uint32_t pins = 0;            // probes (or the uploading put) using the range
     State state = kLive;
   };
@@ -100,7 +107,6 @@ struct adl_bloom_filter_cache {
   uint8_t *arena = nullptr;       // [ones][blocks...]
   uint64_t capacity = 0, used = 0;
   uint32_t max_tables = 0;
-  int32_t bpk = 0;
   std::list<Entry> lru;      // live entries, front = most recently used
   std::list<Entry> limbo;    // loading (pinned by their put) and dead (pinned by probes)
   std::unordered_map<std::string, Iter> index;  // live entries only
@@ -109,6 +115,10 @@ struct adl_bloom_filter_cache {
   // first one; srv_tried: do not retry a failed creation)
   adl_srv::Server *srv = nullptr;
   bool srv_tried = false;
+  // after a kBusy (the server's wave found no room on the GPU for
+  // adl_srv::kTimeout), small batches go straight to a launch until this
+  // steady-clock time (ns), instead of each waiting out the timeout again
+  std::atomic<int64_t> srv_backoff_until{0};
 
   bool alloc(uint64_t size, uint64_t &at) {
     for (auto it = free_.begin(); it != free_.end(); ++it) {
@@ -170,7 +180,6 @@ int adl_bloom_filter_cache_create(uint64_t capacity_bytes, uint32_t max_tables, 
     auto *c = new adl_bloom_filter_cache;
     c->capacity = adl_host::round_up(capacity_bytes, kAlign);
     c->max_tables = max_tables;
-    c->bpk = bits_per_key;
     if (hipMalloc((void **)&c->arena, c->capacity + kAlign) != hipSuccess) {
       (void)hipGetLastError();
       delete c;
@@ -204,7 +213,8 @@ int adl_bloom_filter_cache_put(adl_bloom_filter_cache *c, const char *oid, uint6
   if (!c || !oid || !h_block) return ADL_ERR_INVALID_ARG;
   try {
     std::vector<uint64_t> off;
-    if (int rc = parse_block(h_block, block_len, c->bpk, off)) return rc;
+    uint8_t k = 1;
+    if (int rc = parse_block(h_block, block_len, off, k)) return rc;
     const uint64_t bytes = off.back();  // the bitmap region
     const uint64_t size = adl_host::round_up(bytes + 1, kAlign);
     const std::string key(oid, oid_len);
@@ -233,6 +243,7 @@ int adl_bloom_filter_cache_put(adl_bloom_filter_cache *c, const char *oid, uint6
       e.base = at;
       e.size = size;
       e.off = std::move(off);
+      e.k = k;
       e.pins = 1;
       e.state = adl_bloom_filter_cache::kLoading;
       mine = c->limbo.insert(c->limbo.end(), std::move(e));
@@ -302,14 +313,16 @@ int adl_bloom_filter_cache_probe(adl_bloom_filter_cache *c, const char *const *o
     hipStream_t st = adl_host::sync_stream(stream);
     // 1. under the lock: per listed table, the arena range of its filter
     //    `filter` (the all-ones filter when the table is not cached, an empty
-    //    range when it has no such filter), its entry pinned and marked used
+    //    range when it has no such filter) and its block's k, its entry pinned
+    //    and marked used
     // (per-thread scratch: a single-key Get allocates nothing here)
     thread_local std::vector<uint64_t> be;
-    thread_local std::vector<uint8_t> cached;
+    thread_local std::vector<uint8_t> cached, kt;
     thread_local std::vector<adl_bloom_filter_cache::Iter> pinned;
     thread_local std::string oid_key;
     be.assign(2 * (size_t)num_tables, 0);
     cached.assign(num_tables, 0);
+    kt.assign(num_tables, 1);
     pinned.clear();
     {
       std::lock_guard<std::mutex> g(c->mu);
@@ -323,6 +336,7 @@ int adl_bloom_filter_cache_probe(adl_bloom_filter_cache *c, const char *const *o
         }
         cached[j] = 1;
         adl_bloom_filter_cache::Iter e = it->second;
+        kt[j] = e->k;
         c->lru.splice(c->lru.begin(), c->lru, e);
         ++e->pins;
         pinned.push_back(e);
@@ -345,7 +359,11 @@ int adl_bloom_filter_cache_probe(adl_bloom_filter_cache *c, const char *const *o
     {
       const uint64_t kbytes = h_offsets ? h_offsets[n] - h_offsets[0] : n * (uint64_t)key_stride;
       adl_srv::Server *srv = nullptr;
-      if (adl_srv::eligible(n, kbytes) && adl_host::knobs().probe_server) {
+      const int64_t now_ns = std::chrono::duration_cast<std::chrono::nanoseconds>(
+                                 std::chrono::steady_clock::now().time_since_epoch())
+                                 .count();
+      if (adl_srv::eligible(n, kbytes) && adl_host::knobs().probe_server &&
+          now_ns >= c->srv_backoff_until.load(std::memory_order_relaxed)) {
         std::lock_guard<std::mutex> g(c->mu);
         if (!c->srv_tried) {
           c->srv_tried = true;
@@ -355,13 +373,14 @@ int adl_bloom_filter_cache_probe(adl_bloom_filter_cache *c, const char *const *o
       }
       if (srv) {
         uint64_t rng[2 * adl_srv::kMaxQ];
+        uint8_t kq[adl_srv::kMaxQ];
         const uint64_t a0 = reinterpret_cast<uint64_t>(c->arena);
         for (uint64_t i = 0; i < n; ++i) {
           rng[2 * i] = a0 + be[h_table[i]];
           rng[2 * i + 1] = a0 + be[num_tables + h_table[i]];
+          kq[i] = kt[h_table[i]];
         }
-        int rc = adl_srv::probe(srv, h_keys, h_offsets, key_stride, n, rng, (uint32_t)adl_host::num_probes(c->bpk),
-                                h_out);
+        int rc = adl_srv::probe(srv, h_keys, h_offsets, key_stride, n, rng, kq, h_out);
         if (rc == ADL_OK && adl_host::g_test_faults.take(ADL_TEST_FAULT_CACHE_COMPLETION) >= 0) rc = ADL_ERR_DEVICE;
         // kBusy: no answer in adl_srv::kTimeout (a healthy GPU with no room for
         // the server's wave): probe by a launch below, the ranges still pinned
@@ -371,16 +390,18 @@ int adl_bloom_filter_cache_probe(adl_bloom_filter_cache *c, const char *const *o
           if (h_uncached) *h_uncached = uncached;
           return ADL_OK;
         }
+        c->srv_backoff_until.store(now_ns + kServerBackoffNs, std::memory_order_relaxed);
       }
     }
     // 2. without the lock: stage keys, offsets, table ids and the range table
-    //    in one H2D, one probe launch, one D2H
+    //    and the range and k tables in one H2D, one probe launch, one D2H
     const uint64_t key_bytes = h_offsets ? h_offsets[n] : n * (uint64_t)key_stride;
     const uint64_t off_bytes = h_offsets ? (n + 1) * 8 : 0;
     const uint64_t o_offs = adl_host::round_up(key_bytes + 16, 256);
     const uint64_t o_fid = o_offs + adl_host::round_up(off_bytes, 256);
     const uint64_t o_be = o_fid + adl_host::round_up(n * 4, 256);
-    const uint64_t o_out = o_be + adl_host::round_up(be.size() * 8, 256);
+    const uint64_t o_k = o_be + adl_host::round_up(be.size() * 8, 256);
+    const uint64_t o_out = o_k + adl_host::round_up(num_tables, 256);
     const uint64_t total = o_out + adl_host::round_up(n, 256);
     // A small batch (a single-key Get) is handed over in the thread's mapped
     // buffer: the kernel reads it and writes its answers there directly.
@@ -405,6 +426,7 @@ int adl_bloom_filter_cache_probe(adl_bloom_filter_cache *c, const char *const *o
       if (off_bytes) memcpy(hbuf + o_offs, h_offsets, off_bytes);
       memcpy(hbuf + o_fid, h_table, n * 4);
       memcpy(hbuf + o_be, be.data(), be.size() * 8);
+      if (num_tables) memcpy(hbuf + o_k, kt.data(), num_tables);
       if (spin) memset(hbuf + o_out, 0xff, n);
       if (hbuf == sg.host && hipMemcpyAsync(dbuf, hbuf, o_out, hipMemcpyHostToDevice, st) != hipSuccess)
         rc = ADL_ERR_DEVICE;
@@ -415,7 +437,7 @@ int adl_bloom_filter_cache_probe(adl_bloom_filter_cache *c, const char *const *o
       const uint64_t *d_be = reinterpret_cast<const uint64_t *>(dbuf + o_be);
       rc = adl_host::adl_probe_ranges_device_ev(dbuf, h_offsets ? reinterpret_cast<uint64_t *>(dbuf + o_offs) : nullptr, n,
                                       key_stride, reinterpret_cast<const uint32_t *>(dbuf + o_fid), num_tables,
-                                      c->arena, d_be, d_be + num_tables, c->bpk, dbuf + o_out, st, done);
+                                      c->arena, d_be, d_be + num_tables, dbuf + o_k, dbuf + o_out, st, done);
     }
     if (rc == ADL_OK && hbuf == sg.host &&
         hipMemcpyAsync(hbuf + o_out, dbuf + o_out, n, hipMemcpyDeviceToHost, st) != hipSuccess)

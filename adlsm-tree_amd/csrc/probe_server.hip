@@ -8,9 +8,11 @@
 // serves requests that host threads post into coherent, device-mapped host
 // memory:
 //
-//   slot j (512 B)   queries (<= kMaxQ), k, per query the absolute device range
-//                    [begin, end) of its filter in the cache arena, key offsets
-//                    and key bytes; written by the host thread holding slot j
+//   slot j (512 B)   queries (<= kMaxQ), per query the absolute device range
+//                    [begin, end) of its filter in the cache arena and its k
+//                    (the probe count of the block's own bits_per_key), key
+//                    offsets and key bytes; written by the host thread holding
+//                    slot j
 //   bell[j] (u32)    request sequence number (bit 31: the request is inline),
 //                    written after the request (release); the 64 bells share
 //                    256 bytes, so one wave-wide load polls every slot
@@ -23,7 +25,8 @@
 //                    6.4-6.6 us median (profiles/r05/r05srv_inline_ab.txt;
 //                    sixteen lines, four loads per lane, measured 9.0).  A
 //                    line read while the host was writing it fails its check
-//                    and is read again at the next poll
+//                    (a position-dependent hash of the other 15 words) and is
+//                    read again at the next poll
 //   done[j] (64 B)   word 0: the served sequence number (a restarted kernel's
 //                    starting point); word 1: the low 24 bits of that number
 //                    above the 8 answer bits.  Both in one 8-byte system-scope
@@ -54,6 +57,7 @@
 // stream's work queues behind it on a shared hardware queue (Server::create).
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
+#include <stddef.h>
 #include <stdint.h>
 #include <string.h>
 
@@ -75,22 +79,25 @@ namespace {
 constexpr uint32_t kSlots = 64;      // one per lane of the server wave
 constexpr uint32_t kSlotBytes = 512;
 constexpr uint32_t kGroup = 4;       // slots staged in LDS at a time (2 KiB)
-constexpr uint32_t kHdrBytes = 16;   // seq (unused by the device), n, k, key bytes
+constexpr uint32_t kHdrBytes = 16;   // seq (unused by the device), n, (unused), key bytes
 constexpr uint32_t kInlineSlots = 4;       // slots whose one-query requests can sit in their bell line
 constexpr uint32_t kInlineKeyBytes = 40;
 constexpr uint32_t kInlineBit = 0x80000000u;  // in a bell: the request is in the slot's line
-constexpr uint32_t kLineCheck = 0x5EED5EEDu;  // the XOR of a line's 16 words
+constexpr uint32_t kLineCheck = 0x5EED5EEDu;  // the XOR of line_word_hash over a line's 16 words
 constexpr uint32_t kRangeOff = kHdrBytes;                      // u64 begin, end per query
 constexpr uint32_t kKoffOff = kRangeOff + 16 * adl_srv::kMaxQ;  // u16 offsets, kMaxQ + 1
 constexpr uint32_t kKeyOff = kKoffOff + 2 * (adl_srv::kMaxQ + 8);
 static_assert(kKeyOff % 16 == 0 && kKeyOff + adl_srv::kMaxKeyBytes + 16 <= kSlotBytes, "slot layout");
 
 struct Slot {
-  uint32_t seq, n, k, key_bytes;
+  uint32_t seq, n, unused, key_bytes;
   uint64_t range[2 * adl_srv::kMaxQ];
-  uint16_t koff[adl_srv::kMaxQ + 8];
+  uint16_t koff[adl_srv::kMaxQ + 1];
+  uint8_t kq[adl_srv::kMaxQ];  // per query: k
+  uint8_t pad[2 * (adl_srv::kMaxQ + 8) - 2 * (adl_srv::kMaxQ + 1) - adl_srv::kMaxQ];
   uint8_t keys[kSlotBytes - kKeyOff];
 };
+static_assert(offsetof(Slot, keys) == kKeyOff, "slot layout");
 static_assert(sizeof(Slot) == kSlotBytes, "slot size");
 
 struct Done {
@@ -101,8 +108,11 @@ struct Done {
 static_assert(sizeof(Done) == 64, "done line");
 
 // A one-query request inline in its slot's bell line: check = kLineCheck ^ the
-// XOR of the other 15 words, so a line torn between two requests (read while
-// the host wrote it) fails the check.
+// XOR of line_word_hash(w_i, i) over the other 15 words (the sequence number
+// included).  The hash depends on the word's position and mixes its bits, so
+// a line torn between two requests (read while the host wrote it: new words
+// beside old ones) fails the check unless a 32-bit hash collides -- a plain
+// XOR lets two words that change by the same delta cancel.
 struct Line {
   uint32_t seq;    // the bell value of this request
   uint32_t check;
@@ -131,6 +141,19 @@ struct Area {
   Done done[kSlots];
   Slot slot[kSlots];
 };
+
+// murmur3's finaliser of the word XOR a per-position constant (0 for the
+// check word, which is the result): host and device compute the same.
+__host__ __device__ __forceinline__ uint32_t line_word_hash(uint32_t w, uint32_t i) {
+  if (i == 1) return 0u;
+  uint32_t h = w ^ (0x9E3779B9u * (i + 1u));
+  h ^= h >> 16;
+  h *= 0x85EBCA6Bu;
+  h ^= h >> 13;
+  h *= 0xC2B2AE35u;
+  h ^= h >> 16;
+  return h;
+}
 
 __device__ __forceinline__ uint32_t ld_sys(const uint32_t *p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -169,7 +192,7 @@ __device__ __forceinline__ uint32_t serve_query(uint32_t k, uint64_t b0, uint64_
 __device__ __forceinline__ uint32_t serve_slot_query(const Slot &sl, uint32_t q) {
   const uint32_t ko = min((uint32_t)sl.koff[q], adl_srv::kMaxKeyBytes);
   const uint32_t ke = min(max((uint32_t)sl.koff[q + 1], ko), adl_srv::kMaxKeyBytes);
-  return serve_query(sl.k, sl.range[2 * q], sl.range[2 * q + 1], sl.keys + ko, ke - ko);
+  return serve_query(sl.kq[q], sl.range[2 * q], sl.range[2 * q + 1], sl.keys + ko, ke - ko);
 }
 
 // The request of a line staged in LDS.
@@ -182,7 +205,14 @@ __device__ __forceinline__ uint32_t serve_line(const Line &ln) {
 // lane 8u + q then answers query q of the group's slot u.  The small footprint
 // (2.25 KiB of LDS, 32 VGPRs) lets the wave run beside a build's persistent
 // workgroups, which leave exactly that much of their CU free (bloom_build.hip,
-// kLdsReserveWords): a Get does not wait for a build.
+// kLdsReserveWords): a Get does not wait for a build.  amdgpu_num_vgpr(16) is
+// doubled for gfx950's unified register file (as kPassARegs' 60 -> 120): the
+// code object's .vgpr_count is 32.  Unconstrained the kernel would take 63, so
+// 18 VGPRs spill to scratch (72 B per lane): kernel arguments and loop state,
+// reloaded once per poll and once per served group, from the L1/L2 the wave
+// alone uses.  tools/kernel_resources.py prints both from the built library
+// and tests/test_kernel_resources.py pins them (no other product kernel on the
+// headline, probe or var-len paths spills).
 __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(16))) void probe_server_kernel(
     Area *area, uint64_t idle_ticks, uint64_t life_ticks, uint32_t gen) {
   __shared__ __attribute__((aligned(16))) uint8_t lslot[kGroup][kSlotBytes];
@@ -199,6 +229,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(16))) void probe
   const uint64_t t0 = now_ticks();
   uint64_t last = t0, tprev = t0;
   bool closing = false;
+  uint32_t closing_polls = 0;
   for (;;) {
     const uint64_t tp = now_ticks();  // this poll (diagnostics: the gap since the previous one)
     const uint32_t bell = ld_sys(&area->bell[lane]);
@@ -206,23 +237,26 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(16))) void probe
     // line l / 16
     const uint32_t lw = ld_sys(reinterpret_cast<const uint32_t *>(area->line) + lane);
     bool pend = bell != served;
-    const bool rung = __ballot(pend) != 0;  // (before the line checks)
     if (__ballot(pend && (bell & kInlineBit)) != 0) {
       // some request is inline: the lines into LDS; line i is checked across
       // lanes 16i .. 16i + 15 and judged by lane i
       lline[lane] = lw;
-      uint32_t x = lw;
+      uint32_t x = line_word_hash(lw, lane & 15);
 #pragma unroll
       for (uint32_t o = 1; o < 16; o <<= 1) x ^= (uint32_t)__shfl_xor((int)x, (int)o);
       const uint32_t xi = (uint32_t)__shfl((int)x, (int)(16 * (lane & (kInlineSlots - 1))));
       const uint32_t si = (uint32_t)__shfl((int)lw, (int)(16 * (lane & (kInlineSlots - 1))));
+      const uint32_t ci = (uint32_t)__shfl((int)lw, (int)(16 * (lane & (kInlineSlots - 1)) + 1));
       __syncthreads();
-      if (pend && (bell & kInlineBit)) pend = lane < kInlineSlots && si == bell && xi == kLineCheck;
+      if (pend && (bell & kInlineBit)) pend = lane < kInlineSlots && si == bell && (xi ^ ci) == kLineCheck;
       // (a torn or stale line is read again at the next poll)
     }
+    // a rung bell whose line failed its check: read again, also when closing
+    // (a bounded number of polls: the host writes the line before its bell)
+    const bool torn = __ballot(bell != served && !pend) != 0 && (!closing || ++closing_polls < 4096);
     const uint64_t pm = __ballot(pend);
     if (pm == 0) {
-      if (closing && !rung) break;  // (a torn line of the last poll is read again)
+      if (closing && !torn) break;
       const uint64_t t = tp;
       tprev = tp;
       const bool stop = __ballot(ld_sys(&area->ctl.stop[lane & 15]) != 0) != 0;
@@ -294,7 +328,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(16))) void probe
     if (pend) served = bell;
     last = now_ticks();
     tprev = tp;
-    if (closing) break;
+    if (closing && !torn) break;
   }
   // the last poll's answers are out: the host may launch the next kernel (on
   // the other stream) as soon as it sees this
@@ -327,6 +361,7 @@ struct Server {
   std::atomic<uint32_t> next_slot{0};
   uint64_t id = 0;  // unique per server of this process (a thread's slot is per server)
   uint64_t idle_ticks = 0, life_ticks = 0;
+  bool debug = false;  // ADL_BLOOM_DEBUG at creation (the launcher thread must not read knobs() while a reload runs)
   // The launcher thread keeps one successor queued behind the running kernel
   // while requests come in, so a kernel that reaches its life limit hands
   // over to the next with no host call on any request's path (a launch call
@@ -390,7 +425,7 @@ int launch_next(Server *s) {
   const auto tl1 = std::chrono::steady_clock::now();
   if (hipGetLastError() != hipSuccess || hipEventRecord(s->exited[gen % Server::kEvents], s->stream) != hipSuccess)
     return ADL_ERR_DEVICE;
-  if (adl_host::knobs().debug) {
+  if (s->debug) {
     const double us_launch = std::chrono::duration<double, std::micro>(tl1 - tl0).count();
     if (us_launch > 50.0) fprintf(stderr, "adl_bloom server: launch call of generation %u took %.1f us\n", gen, us_launch);
   }
@@ -519,6 +554,7 @@ Server *create() {
   // wave to start: profiles/r05/r05m_coexist_life.txt.)
   s->idle_ticks = adl_host::knobs().server_idle_us * 100;
   s->life_ticks = adl_host::knobs().server_life_us * 100;
+  s->debug = adl_host::knobs().debug;
   try {
     s->launcher = std::thread(launcher_main, s);
   } catch (...) {
@@ -558,13 +594,21 @@ bool eligible(uint64_t n, uint64_t key_bytes) { return n >= 1 && n <= kMaxQ && k
 
 uint64_t launches() { return g_launches.load(std::memory_order_relaxed); }
 
+uint32_t resident_servers() {
+  std::lock_guard<std::mutex> g(g_reg_mu);
+  uint32_t r = 0;
+  if (g_reg)
+    for (const Server *s : *g_reg) r += __atomic_load_n(&s->host->ctl.alive, __ATOMIC_ACQUIRE) != 0;
+  return r;
+}
+
 uint32_t live_servers() {
   std::lock_guard<std::mutex> g(g_reg_mu);
   return g_reg ? (uint32_t)g_reg->size() : 0u;
 }
 
 int probe(Server *s, const uint8_t *h_keys, const uint64_t *h_offsets, uint32_t key_stride, uint64_t n,
-          const uint64_t *range, uint32_t k, uint8_t *h_out) {
+          const uint64_t *range, const uint8_t *kq, uint8_t *h_out) {
   const uint64_t key_bytes = h_offsets ? h_offsets[n] - h_offsets[0] : n * (uint64_t)key_stride;
   if (!s || !eligible(n, key_bytes)) return ADL_ERR_INVALID_ARG;
   // a slot per thread and server (round-robin); threads beyond kSlots share
@@ -581,31 +625,31 @@ int probe(Server *s, const uint8_t *h_keys, const uint64_t *h_offsets, uint32_t 
   s->seq[my] = (s->seq[my] + 1) & ~kInlineBit;
   if (s->seq[my] == 0) s->seq[my] = 1;
   const bool inl = my < kInlineSlots && n == 1 && key_bytes <= kInlineKeyBytes && range[1] >= range[0] &&
-                   range[1] - range[0] <= 0xFFFFFFFFull && k < 256;
+                   range[1] - range[0] <= 0xFFFFFFFFull;
   const uint32_t seq = s->seq[my] | (inl ? kInlineBit : 0u);
   const uint8_t *kp = h_keys + (h_offsets ? h_offsets[0] : 0);
   if (inl) {
     // the whole line, check word last computed, in one copy; then the bell
     Line ln{};
     ln.seq = seq;
-    ln.k_klen = k | (uint32_t)key_bytes << 8;
+    ln.k_klen = kq[0] | (uint32_t)key_bytes << 8;
     ln.len = (uint32_t)(range[1] - range[0]);
     ln.begin = range[0];
     memcpy(ln.key, kp, key_bytes);
     uint32_t w[16];
     memcpy(w, &ln, sizeof(ln));
     uint32_t x = kLineCheck;
-    for (uint32_t i = 0; i < 16; ++i) x ^= i == 1 ? 0u : w[i];
+    for (uint32_t i = 0; i < 16; ++i) x ^= line_word_hash(w[i], i);
     ln.check = x;
     memcpy(&s->host->line[my], &ln, sizeof(ln));
   } else {
     Slot &sl = s->host->slot[my];
     sl.n = (uint32_t)n;
-    sl.k = k;
     sl.key_bytes = (uint32_t)key_bytes;
     for (uint64_t q = 0; q < n; ++q) {
       sl.range[2 * q] = range[2 * q];
       sl.range[2 * q + 1] = range[2 * q + 1];
+      sl.kq[q] = kq[q];
       sl.koff[q] = (uint16_t)(h_offsets ? h_offsets[q] - h_offsets[0] : q * key_stride);
     }
     sl.koff[n] = (uint16_t)key_bytes;
@@ -647,7 +691,7 @@ int probe(Server *s, const uint8_t *h_keys, const uint64_t *h_offsets, uint32_t 
     }
     if (since() > kTimeout) return kBusy;
   }
-  if (adl_host::knobs().debug) {
+  if (s->debug) {
     // ADL_BLOOM_DEBUG: where a slow request spent its time
     const auto t1 = std::chrono::steady_clock::now();
     const double us_ring = std::chrono::duration<double, std::micro>(t0 - tb).count();

@@ -26,15 +26,20 @@ __attribute__((visibility("hidden"))) Server *create();
 __attribute__((visibility("hidden"))) void destroy(Server *s);
 __attribute__((visibility("hidden"))) bool eligible(uint64_t n, uint64_t key_bytes);
 // n queries (keys by offsets or fixed stride), query q against the device
-// byte range [range[2q], range[2q+1]) of k-probe filter bits; answers to
-// h_out.  Returns ADL_* status, or kBusy when no answer came within kTimeout.
+// byte range [range[2q], range[2q+1]) of kq[q]-probe filter bits (each table's
+// block carries its own bits_per_key); answers to h_out.  Returns ADL_*
+// status, or kBusy when no answer came within kTimeout.
 __attribute__((visibility("hidden"))) int probe(Server *s, const uint8_t *h_keys, const uint64_t *h_offsets,
-                                                uint32_t key_stride, uint64_t n, const uint64_t *range, uint32_t k,
-                                                uint8_t *h_out);
+                                                uint32_t key_stride, uint64_t n, const uint64_t *range,
+                                                const uint8_t *kq, uint8_t *h_out);
 
-// Servers that exist in this process (created, not destroyed): the build then
-// leaves every CU a wave slot for their kernel (bloom_build.hip, pass B).
+// Servers that exist in this process (created, not destroyed).
 __attribute__((visibility("hidden"))) uint32_t live_servers();
+// Servers whose kernel is resident or about to start (the alive word: set by
+// the host before a launch and by the kernel as it starts, cleared by the
+// kernel as it leaves).  The build takes its items from work queues only
+// then (bloom_build.hip, ADL_BLOOM_BUILD_QUEUES).
+__attribute__((visibility("hidden"))) uint32_t resident_servers();
 
 // Server kernels launched by this process so far (relaunches after the idle
 // and life limits included); readpath_test's tail-latency run reports it.

@@ -2,7 +2,8 @@
 //  under concurrency, and its latency.  Needs a GPU.
 //
 //   readpath_test <outdir> [threads] [rounds]
-//     Builds a level of T SSTable filter blocks (FilterBlockWriter, GPU),
+//     Builds a level of T SSTable filter blocks (FilterBlockWriter, GPU; the
+//     tables' bits_per_key cycle through 10, 3 and 16),
 //     caches them in a FilterCache by oid, and runs the level multi-get
 //     (LevelMultiGetFilter: Level::Get's candidate tables, src/revision.cpp:
 //     265-310, and SSTableReader::Get's filter check, src/sstable.cpp:238,
@@ -76,11 +77,15 @@ struct Level {
   std::vector<std::string> blocks;
 };
 
-// table t holds user keys [t * stride, t * stride + span) with seq = key index
-Level BuildLevel(int T, uint64_t stride, uint64_t span, RC *rc) {
+// table t holds user keys [t * stride, t * stride + span) with seq = key
+// index.  mixed: table t is written with bits_per_key {10, 3, 16}[t % 3] (a DB
+// reopened with another DBOptions::bits_per_key, src/options.hpp:24, keeps
+// its older tables: one level, one cache, several k)
+Level BuildLevel(int T, uint64_t stride, uint64_t span, RC *rc, bool mixed = false) {
   Level lv;
   for (int t = 0; t < T; ++t) {
-    FilterBlockWriter w(std::make_unique<BloomFilter>(kBpk));
+    static const int kMixed[3] = {10, 3, 16};
+    FilterBlockWriter w(std::make_unique<BloomFilter>(mixed ? kMixed[t % 3] : kBpk));
     const uint64_t lo = (uint64_t)t * stride, hi = lo + span;
     for (uint64_t i = lo; i < hi; ++i) w.Update(UserKey(i));
     std::string block;
@@ -467,7 +472,7 @@ int main(int argc, char **argv) {
   const int T = 24;
   const uint64_t stride = 5000, span = 20000;
   RC rc;
-  Level lv = BuildLevel(T, stride, span, &rc);
+  Level lv = BuildLevel(T, stride, span, &rc, /*mixed=*/true);
   if (rc) {
     fprintf(stderr, "build failed: %s\n", std::string(strrc(rc)).c_str());
     return 1;

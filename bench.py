@@ -24,8 +24,10 @@ Multi-GPU: one process per GPU (torch.distributed.run).  No workload has a
 collective on its data path -- each rank owns whole filters.  RCCL reduces the
 key counter (sum) and the elapsed time (max).  The default workload also
 reports configs[3] as a `compaction_strong` sub-record (256 tables split over
-the N GPUs, strong scaling), the north star's multi-GPU target.  Rank 0
-prints one JSON line.
+the N GPUs, strong scaling), the north star's multi-GPU target, the same
+build in a process serving Gets (`headline_with_reader`), and configs[4] and
+configs[2] as `probe` and `varlen` sub-records, each with its own parity,
+roofline and CPU baseline.  Rank 0 prints one JSON line.
 """
 import argparse
 import hashlib
@@ -60,6 +62,10 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget")
     ap.add_argument("--no-compaction-strong", action="store_true",
                     help="single: skip the configs[3] compaction_strong sub-record")
+    ap.add_argument("--no-sub-records", action="store_true",
+                    help="single: skip the configs[4] probe and configs[2] varlen sub-records")
+    ap.add_argument("--no-reader", action="store_true",
+                    help="single: skip the headline_with_reader record")
     return ap.parse_args()
 
 
@@ -665,35 +671,30 @@ def lds_roofline(workload, kernels_us):
     return out
 
 
-def main():
-    args = parse()
+_STREAM_GBS = []
+
+
+def stream_gbs_once():
+    """hbm_stream_read_gbs, measured once per process (every record reuses it)."""
+    if not _STREAM_GBS:
+        _STREAM_GBS.append(hbm_stream_read_gbs())
+    return _STREAM_GBS[0]
+
+
+def measure(kind, args, rank, world, backend, barrier, timed, sub=False):
+    """One workload's record: warmup, the timed K steps (the throughput), the
+    same K steps again with per-kernel HIP events (the roofline), parity
+    against the reference / oracle pins, and (rank 0, one GPU) its CPU
+    baseline.  All ranks call; rank 0 gets the dict, the others None.
+    sub: a sub-record of the default line (smaller CPU-baseline budget, no
+    e2e)."""
     import torch
-    import torch.distributed as dist
 
     import adlbloom as ab
+    from adlbloom import dist as D
 
-    rank = int(os.environ.get("RANK", 0))
-    world = int(os.environ.get("WORLD_SIZE", 1))
-    local = int(os.environ.get("LOCAL_RANK", 0))
-    if world != args.gpus:
-        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
-    if not torch.cuda.is_available():
-        raise SystemExit("bench.py needs a GPU")
-    torch.cuda.set_device(local)
-    backend = None
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        world = dist.get_world_size()
-        backend = dist.get_backend()
-
-    def barrier():
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-
-    w = Workload(args.workload, rank, args.keys, world, args.queries)
-    probe = args.workload == "probe"
+    w = Workload(kind, rank, args.keys, world, args.queries)
+    probe = kind == "probe"
     torch.cuda.synchronize()
     for _ in range(args.warmup):
         w.step()
@@ -726,20 +727,7 @@ def main():
         w.bytes_per_launch = ALGO_BYTES_PER_QUERY * w.served
 
     # RCCL: the only collective -- sum of keys built, max of elapsed time
-    from adlbloom import dist as D
-
     total_keys, elapsed_max = D.reduce_throughput(float(w.n) * args.steps, elapsed, device="cuda")
-
-    def timed(fn, steps, warmup=2):
-        """max over ranks of the wall time of `steps` calls, barriers on both sides"""
-        for _ in range(warmup):
-            fn()
-        barrier()
-        t = time.perf_counter()
-        for _ in range(steps):
-            fn()
-        barrier()
-        return D.reduce_throughput(0.0, time.perf_counter() - t, device="cuda")[1]
 
     # the routed probe (N > 1), reported beside the owner-bucketed measurement
     routing_variant = None
@@ -751,45 +739,30 @@ def main():
             "value": round(w.total_queries * args.steps / el / 1e6, 1), "unit": "Mqueries/s",
             "ms_per_step": round(el / max(args.steps, 1) * 1e3, 4), "rank0_traffic": w.routing}
 
-    parity = None
-    if rank == 0 and args.workload == "single":
+    if rank == 0 and kind == "single":
         parity = parity_check(out, w.n, w.keys)
     elif probe:
         parity = probe_check(w, out, rank, world)
     else:
         parity = build_parity(w, rank)
 
-    # configs[3] beside the headline: the north star's multi-GPU target (256
-    # tables split over the N GPUs, strong scaling), its own clock
-    comp_strong = None
-    if args.workload == "single" and not args.no_compaction_strong:
-        wc = Workload("compaction", rank, 0, world)
-        el = timed(wc.step, args.steps)
-        tot = D.reduce_throughput(float(wc.n) * args.steps, 0.0, device="cuda")[0]
-        comp_strong = {"metric": "Mkeys/s bloom-filter build (device-resident), 16B keys, bits/key=10, "
-                                 "configs[3]: 256 SSTables x 1M keys split over the GPUs",
-                       "value": round(tot / el / 1e6, 1), "unit": "Mkeys/s",
-                       "ms_per_step": round(el / max(args.steps, 1) * 1e3, 4), "steps": args.steps,
-                       "scaling": "strong", "tables_total": COMPACTION_TABLES, "tables_per_gpu": len(wc.tables),
-                       "parity": build_parity(wc, rank)}
-        if rank == 0 and not args.no_cpu_baseline:
-            # every N: the reference's filter builds on this host's cores for the same tables
-            comp_strong["cpu_baseline"] = cpu_baseline(min(args.cpu_seconds, 5.0), "compaction", wc)
-        del wc
-        torch.cuda.empty_cache()
-
+    rec = None
     if rank == 0:
         if probe:
             kern_ms = probe_ms
             kernels = {"probe (adl_bloom_probe_batch_device)": round(probe_ms * 1e3, 2)}
             kname = ("adl_bloom_probe_batch_device: tile-binned pipeline pb_* (9 launches) for large 16-byte "
                      "batches, bloom_probe_multi_kernel otherwise")
+            med = None
         else:
             # kernel time per step (every filter of a segmented build in one launch pair)
             kern_ms = (ms_a + ms_b) / max(args.steps, 1)
             kernels = {"bloom_bin_kernel": round(ms_a / max(args.steps, 1) * 1e3, 2),
                        "bloom_tile_kernel": round(ms_b / max(args.steps, 1) * 1e3, 2)}
             kname = "bloom_bin_kernel + bloom_tile_kernel (one build = the pair)"
+            if kind == "varlen":
+                kname = ("hash_var_kernel + bloom_bin16_kernel<SrcH> (the pass-A interval) + bloom_tile_kernel "
+                         "(one build)")
             # median over the steps: each step's launch pairs summed
             per = len(pairs) // max(args.steps, 1)
             if per and len(pairs) == per * args.steps:
@@ -800,19 +773,22 @@ def main():
                        "build": round(float(np.median([x[0] + x[1] for x in steps_ms])) * 1e3, 2)}
             else:
                 med = None
-        timed = kern_ms > 0 and (probe or nb)
-        achieved = w.bytes_per_launch / (kern_ms * 1e-3) / 1e9 if timed else None
-        traffic = load_traffic(args.workload, w.bytes_per_launch)
-        stream_gbs = hbm_stream_read_gbs()
+        is_timed = kern_ms > 0 and (probe or nb)
+        achieved = w.bytes_per_launch / (kern_ms * 1e-3) / 1e9 if is_timed else None
+        traffic = load_traffic(kind, w.bytes_per_launch)
+        stream_gbs = stream_gbs_once()
         if probe:
             metric = "Mqueries/s bloom-filter probe (device-resident), 16B keys, 256 filters, bits/key=10"
             if world > 1:
                 metric += ", owner-bucketed"
-        elif args.workload == "varlen":
+        elif kind == "varlen":
             metric = "Mkeys/s bloom-filter build (device-resident), var-len keys, bits/key=10"
+        elif kind == "compaction":
+            metric = ("Mkeys/s bloom-filter build (device-resident), 16B keys, bits/key=10, "
+                      "configs[3]: 256 SSTables x 1M keys")
         else:
             metric = "Mkeys/s bloom-filter build (device-resident), 16B keys, bits/key=10"
-        out_json = {
+        rec = {
             "metric": metric,
             "value": round(total_keys / elapsed_max / 1e6, 1),
             "unit": "Mqueries/s" if probe else "Mkeys/s",
@@ -822,7 +798,7 @@ def main():
             "ms_per_step": round(elapsed_max / max(args.steps, 1) * 1e3, 4),
             "ms_per_step_kernel_timed": round(elapsed_instrumented / max(args.steps, 1) * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "strong" if args.workload in ("probe", "compaction") else "weak",
+            "scaling": "strong" if kind in ("probe", "compaction") else "weak",
             "vs_baseline": None,
             "dtype": w.dtype,
             "data": "synthetic (SplitMix64 keys generated on device, SURVEY.md §8d)",
@@ -840,52 +816,183 @@ def main():
                                  "pipeline), over a second pass of the same K steps right after the timed one",
                 "algorithmic_bytes_per_step": w.bytes_per_launch,
                 "us_per_step": kernels,
-                "median_us_per_step": None if probe else med,
+                "median_us_per_step": med,
                 "zero_fill_us": None if probe else 0.0,  # none: pass B writes every bitmap byte
                 "launch_pairs_per_build": None if probe else round(nb / max(args.steps, 1), 2),
                 "read_only_frac": round(16 * w.n / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
-                if (timed and args.workload in ("single", "compaction")) else None,
+                if (is_timed and kind in ("single", "compaction")) else None,
                 "measured_stream_read_gbs": stream_gbs,
                 "frac_of_measured_stream_read": round(achieved / stream_gbs, 4) if (achieved and stream_gbs) else None,
             },
             "parity": parity,
         }
-        if probe and parity and timed:
+        if traffic and is_timed:
+            rec["roofline"]["traffic_gbs"] = round(traffic / (kern_ms * 1e-3) / 1e9, 1)
+            rec["roofline"]["traffic_over_algorithmic"] = round(traffic / w.bytes_per_launch, 3)
+        if probe and parity and is_timed:
             # what the direct kernel (one query per lane, random bitmap reads) would be
             # bound by: the measured random-read rate over the same 2.56 GB arena, at the
             # reference's early-exit read count; the binned pipeline replaces those reads
             rr = hbm_random_read_gps(w.bitmaps)
-            out_json["roofline"]["random_reads"] = {
+            rec["roofline"]["random_reads"] = {
                 "reads_per_query_direct_kernel": parity["bitmap_reads_per_query"],
                 "measured_random_read_greads_per_s": rr,
                 "direct_kernel_ceiling_mqueries_per_s": round(rr * 1e3 / parity["bitmap_reads_per_query"], 1)
                 if rr else None,
                 "working_set_bytes": int(w.bitmaps.numel()),
             }
-        if traffic and timed:
-            out_json["roofline"]["traffic_gbs"] = round(traffic / (kern_ms * 1e-3) / 1e9, 1)
         if probe and w.bucketing_ms is not None:
-            out_json["probe_bucketing_ms"] = round(w.bucketing_ms, 2)
+            rec["probe_bucketing_ms"] = round(w.bucketing_ms, 2)
         if not probe:
-            out_json["roofline"]["alu"] = alu_roofline(args.workload, w.n, kernels)
-            out_json["roofline"]["lds"] = lds_roofline(args.workload, kernels)
+            rec["roofline"]["alu"] = alu_roofline(kind, w.n, kernels)
+            rec["roofline"]["lds"] = lds_roofline(kind, kernels)
             pos = w.builder.positions()
-            out_json["roofline"]["positions_per_build"] = {
+            rec["roofline"]["positions_per_build"] = {
                 "positions": pos, "per_key": round(pos / w.n, 3),
                 "round_trip_bytes": 8 * pos,  # 4 B written by pass A, read by pass B
                 "note": "k bit-sets per key, less the keys whose hash pair their workgroup had already counted"}
         if routing_variant:
-            out_json["roofline"]["routing_variant"] = routing_variant
-        if comp_strong:
-            out_json["compaction_strong"] = comp_strong
-        if world == 1 and args.workload == "single" and not args.no_e2e:
-            out_json["e2e"] = e2e(w.n)
-        if world == 1 and args.workload == "compaction" and not args.no_e2e:
-            out_json["e2e"] = e2e_compaction(w)
+            rec["roofline"]["routing_variant"] = routing_variant
+        if world == 1 and kind == "single" and not args.no_e2e and not sub:
+            rec["e2e"] = e2e(w.n)
+        if world == 1 and kind == "compaction" and not args.no_e2e and not sub:
+            rec["e2e"] = e2e_compaction(w)
         if world == 1 and not args.no_cpu_baseline:
-            out_json["cpu_baseline"] = cpu_baseline(args.cpu_seconds, args.workload, w)
+            rec["cpu_baseline"] = cpu_baseline(min(args.cpu_seconds, 5.0) if sub else args.cpu_seconds, kind, w)
         else:
-            out_json["cpu_baseline"] = None
+            rec["cpu_baseline"] = None
+    del w
+    torch.cuda.empty_cache()
+    return rec
+
+
+def with_reader(args, rank, world, timed):
+    """The headline build in a process that serves Gets: a
+    FilterCache with one table whose single-key probe has launched the
+    resident probe server.  Two timings of the same K builds: right after a
+    Get (the server's wave resident on one CU: the build takes its items from
+    work queues) and after the server's 2 ms idle limit has passed (no
+    kernel resident: the static order, as in a process with no reader)."""
+    import torch
+
+    import adlbloom as ab
+
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+
+    keys = O.splitmix_keys16(0x7AB1E, 20_000)
+    blk = O.filter_block_final([O.keys2block(keys, bits_per_key=BPK).tobytes()], BPK)
+    cache = ab.FilterCache(8 << 20, max_tables=4)
+    cache.put(b"reader-table", blk)
+    get = lambda: cache.probe([b"reader-table"], np.zeros(1, np.uint32), keys[:1])  # noqa: E731
+    w = Workload("single", rank, args.keys, world)
+    for _ in range(args.warmup):
+        w.step()
+    torch.cuda.synchronize()
+    launches0 = ab.probe_server_launches()
+
+    def resident_step():
+        # a Get before every build keeps the server's kernel resident (its
+        # idle limit is 2 ms) while the build runs
+        got, _ = get()
+        assert got[0] == 1
+        w.step()
+
+    def idle_step():
+        w.step()
+
+    el_res = timed(resident_step, args.steps)
+    got, _ = get()
+    time.sleep(0.02)  # past the server's idle limit: its kernel leaves
+    el_idle = timed(idle_step, args.steps)
+    launches = ab.probe_server_launches() - launches0
+    cache.close()
+    parity = parity_check(w.builder.bitmap[:w.builder.nbytes], w.n, w.keys) if rank == 0 else None
+    del w
+    torch.cuda.empty_cache()
+    return {"server_resident": {"ms_per_step": round(el_res / max(args.steps, 1) * 1e3, 4),
+                                "note": "one single-key Get (resident probe server) before each build, the "
+                                        "Get's own time (~7 us) included"},
+            "reader_idle": {"ms_per_step": round(el_idle / max(args.steps, 1) * 1e3, 4),
+                            "note": "the same builds after the server's idle exit, in the same process"},
+            "server_launches": int(launches), "parity": parity}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
+    if not torch.cuda.is_available():
+        raise SystemExit("bench.py needs a GPU")
+    torch.cuda.set_device(local)
+    backend = None
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        world = dist.get_world_size()
+        backend = dist.get_backend()
+
+    from adlbloom import dist as D
+
+    def barrier():
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    def timed(fn, steps, warmup=2):
+        """max over ranks of the wall time of `steps` calls, barriers on both sides"""
+        for _ in range(warmup):
+            fn()
+        barrier()
+        t = time.perf_counter()
+        for _ in range(steps):
+            fn()
+        barrier()
+        return D.reduce_throughput(0.0, time.perf_counter() - t, device="cuda")[1]
+
+    out_json = measure(args.workload, args, rank, world, backend, barrier, timed)
+
+    if args.workload == "single":
+        # configs[3] beside the headline: the north star's multi-GPU target (256
+        # tables split over the N GPUs, strong scaling), its own clock
+        if not args.no_compaction_strong:
+            wc = Workload("compaction", rank, 0, world)
+            el = timed(wc.step, args.steps)
+            tot = D.reduce_throughput(float(wc.n) * args.steps, 0.0, device="cuda")[0]
+            comp_strong = {"metric": "Mkeys/s bloom-filter build (device-resident), 16B keys, bits/key=10, "
+                                     "configs[3]: 256 SSTables x 1M keys split over the GPUs",
+                           "value": round(tot / el / 1e6, 1), "unit": "Mkeys/s",
+                           "ms_per_step": round(el / max(args.steps, 1) * 1e3, 4), "steps": args.steps,
+                           "scaling": "strong", "tables_total": COMPACTION_TABLES, "tables_per_gpu": len(wc.tables),
+                           "parity": build_parity(wc, rank)}
+            if rank == 0 and not args.no_cpu_baseline:
+                # every N: the reference's filter builds on this host's cores for the same tables
+                comp_strong["cpu_baseline"] = cpu_baseline(min(args.cpu_seconds, 5.0), "compaction", wc)
+            del wc
+            torch.cuda.empty_cache()
+            if rank == 0:
+                out_json["compaction_strong"] = comp_strong
+        if not args.no_reader:
+            wr = with_reader(args, rank, world, timed)
+            if rank == 0:
+                head = out_json["ms_per_step"]
+                for k in ("server_resident", "reader_idle"):
+                    wr[k]["value"] = round(args.keys * world / (wr[k]["ms_per_step"] * 1e-3) / 1e6, 1)
+                    wr[k]["vs_headline"] = round(wr[k]["ms_per_step"] / head - 1.0, 4)
+                out_json["headline_with_reader"] = wr
+        # configs[4] and configs[2] on the driver's default run (VERDICT r5 #2)
+        for kind in ([] if args.no_sub_records else ["probe", "varlen"]):
+            rec = measure(kind, args, rank, world, backend, barrier, timed, sub=True)
+            if rank == 0:
+                out_json[kind] = rec
+
+    if rank == 0:
         print(json.dumps(out_json), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -265,7 +265,12 @@ int adl_bloom_filter_set_destroy(adl_bloom_filter_set *set);
  * capacity_bytes, keyed by oid (any byte string, e.g. the SHA-256 file name),
  * least recently used evicted first, at most max_tables blocks: the filter
  * side of DB::table_cache_ (src/db.hpp:96-97, LRUCache src/cache.hpp:23-93).
- * Every block must carry bits_per_key.  Thread-safe (one mutex per cache). */
+ * Blocks of any bits_per_key share one cache: each is probed with the k of
+ * its own "bf:" info, as FilterBlockReader::CreateFilterAlgorithm reads it per
+ * block (src/filter_block.cpp:158-170), so a level of tables written under
+ * different DBOptions::bits_per_key is served by one cache and one launch.
+ * bits_per_key (>= 0) is kept for source compatibility and not otherwise
+ * used.  Thread-safe (one mutex per cache). */
 typedef struct adl_bloom_filter_cache adl_bloom_filter_cache;
 
 int adl_bloom_filter_cache_create(uint64_t capacity_bytes, uint32_t max_tables, int32_t bits_per_key,
@@ -273,9 +278,9 @@ int adl_bloom_filter_cache_create(uint64_t capacity_bytes, uint32_t max_tables, 
 int adl_bloom_filter_cache_destroy(adl_bloom_filter_cache *cache);
 
 /* Insert (or replace) the filter block of table `oid`: validated as
- * FilterBlockReader::Init does (ADL_FILTER_BLOCK_ERROR), ADL_ERR_INVALID_ARG if
- * its bits_per_key differs from the cache's; its bitmaps are uploaded once
- * and it becomes the most recently used.  Synchronous. */
+ * FilterBlockReader::Init does (ADL_FILTER_BLOCK_ERROR); its bitmaps are
+ * uploaded once, its k taken from its own bits_per_key, and it becomes the
+ * most recently used.  Synchronous. */
 int adl_bloom_filter_cache_put(adl_bloom_filter_cache *cache, const char *oid, uint64_t oid_len,
                                const uint8_t *h_block, uint64_t block_len);
 

@@ -653,11 +653,18 @@ def test_filter_cache_lru_and_errors(dev, ab, oracle):
     for t in range(3):
         small.put(b"s%d" % t, blocks[t])
     assert small.stats()[0] == 2 and b"s0" not in small
-    # FilterBlockReader::Init's errors; a block of another bits_per_key
+    # FilterBlockReader::Init's errors
     assert cache.put_status(b"bad", b"\x00\x01") == ab.ADL_FILTER_BLOCK_ERROR
     assert cache.put_status(b"bad", blocks[0][:-3]) == ab.ADL_FILTER_BLOCK_ERROR
-    other = oracle.filter_block_final([oracle.keys2block(oracle.splitmix_keys16(1, 100), bits_per_key=12).tobytes()], 12)
-    assert cache.put_status(b"bpk", other) == -1
+    # a block of another bits_per_key is accepted and probed with its own k
+    # (the reference reads bpk per block, src/filter_block.cpp:158-170)
+    k12 = oracle.splitmix_keys16(1, 3000)
+    bm12 = oracle.keys2block(k12, bits_per_key=12)
+    other = oracle.filter_block_final([bm12.tobytes()], 12)
+    assert cache.put_status(b"bpk", other) == 0
+    q12 = np.concatenate([k12[:500], oracle.splitmix_keys16(2, 2000)])
+    got, unc = cache.probe([b"bpk"], np.zeros(len(q12), np.uint32), q12)
+    assert unc == 0 and np.array_equal(got, oracle.probe(q12, bm12, bits_per_key=12))
     # the reference test scenario's block: both filters probed through the cache
     b0 = [b"hello", b"world", b"hello-yly", b"hello-ddl"] + [b"hello-ddl%d" % i for i in range(10000)]
     b1 = [b"adl", b"dont", b"like-apple"]

@@ -43,9 +43,15 @@ def ab():
     return adlbloom
 
 
-def test_level_multiget_threaded_vs_oracle(dev, oracle, tmp_path):
+@pytest.mark.parametrize("server", ["1", "0"])
+def test_level_multiget_threaded_vs_oracle(dev, oracle, tmp_path, server):
+    """The level's tables are written with bits_per_key 10, 3 and 16 in turn
+    and share one cache: every answer is checked against the oracle with each
+    block's own bits_per_key.  server=0 sends the single-key IsKeyExists calls
+    through a launched probe instead of the resident server."""
     exe = os.path.join(ROOT, "adlsm-tree_amd", "bin", "readpath_test")
-    r = subprocess.run([exe, str(tmp_path), "8", "10"], capture_output=True, text=True, timeout=600)
+    r = subprocess.run([exe, str(tmp_path), "8", "10" if server == "1" else "4"], capture_output=True, text=True,
+                       timeout=600, env=dict(os.environ, ADL_BLOOM_PROBE_SERVER=server))
     assert r.returncode == 0, r.stdout + r.stderr
     assert "phase 1 (level cached) 0 mismatches" in r.stdout and "phase 2 (evicting) 0 mismatches" in r.stdout
 
@@ -70,6 +76,7 @@ def test_level_multiget_threaded_vs_oracle(dev, oracle, tmp_path):
     assert len(got) == len(queries)
     # every table's filter 0 over every query, by the oracle
     want_bits = []
+    assert sorted({rd.bits_per_key for rd in readers}) == [3, 10, 16]
     for rd in readers:
         o1, o2 = rd.filter_range(0)
         bm = np.frombuffer(rd.block[o1:o2], dtype=np.uint8)
@@ -324,6 +331,51 @@ def test_probe_server_single_keys_vs_oracle(dev, ab, oracle, knobs, bpk):
         assert np.array_equal(got3, (table == T).astype(np.uint8))
         checked += n
     assert checked > 1500
+    cache.close()
+
+
+def test_filter_cache_mixed_bpk(dev, ab, oracle, knobs):
+    """Tables written with bits_per_key 3, 10 and 16 in ONE cache: multi-get
+    batches (one launch: a k per table), single-key and small batches through
+    the resident server (a k per query) and through a launched probe, all equal
+    to the oracle with each block's own bits_per_key (the reference builds the
+    BloomFilter of each block from its "bf:" info, src/filter_block.cpp:158-170;
+    Level::Get reads every table of a level, src/revision.cpp:265-310)."""
+    bpks = [3, 10, 16, 3, 16, 10]
+    tabs = [_varlen_block(oracle, 70 + t, 2500, b) for t, b in enumerate(bpks)]
+    cache = ab.FilterCache(16 << 20, max_tables=8)
+    oids = [b"mix-%d" % t for t in range(len(bpks))]
+    for o, (_, blk, _) in zip(oids, tabs):
+        cache.put(o, blk)
+    T = len(bpks)
+
+    def want_of(qs, table):
+        data, offs = _pack(qs)
+        return np.array([int(oracle.probe(data, tabs[t][2], offsets=offs[i:i + 2].copy(), bits_per_key=bpks[t])[0])
+                         for i, t in enumerate(table)], np.uint8)
+
+    rng = np.random.default_rng(77)
+    # a large batch: one launch
+    n = 6000
+    table = rng.integers(0, T, n).astype(np.uint32)
+    qs = [tabs[t][0][int(rng.integers(0, 2500))] if i % 2 else
+          rng.integers(0, 256, int(rng.integers(0, 40)), dtype=np.uint8).tobytes() for i, t in enumerate(table)]
+    want = want_of(qs, table)
+    data, offs = _pack(qs)
+    got, unc = cache.probe(oids, table, data, offs)
+    assert unc == 0 and np.array_equal(got, want)
+    assert 0 < int(want.sum()) < n
+    # small batches: the server (per-query k), then launched
+    for server in ("1", "0"):
+        knobs.set("ADL_BLOOM_PROBE_SERVER", server)
+        for it in range(240):
+            m = 1 + it % 8
+            sel = rng.integers(0, n, m)
+            sub = [qs[int(i)] for i in sel]
+            d, o = _pack(sub)
+            got, _ = cache.probe(oids, table[sel], d, o)
+            assert np.array_equal(got, want[sel]), (server, it)
+    knobs.unset("ADL_BLOOM_PROBE_SERVER")
     cache.close()
 
 
