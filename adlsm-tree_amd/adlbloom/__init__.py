@@ -47,6 +47,7 @@ EXPORTS = (
     "adl_bloom_profile_each", "adl_bloom_probe_batch_workspace_bytes", "adl_bloom_probe_batch_device",
     "adl_bloom_test_fault", "adl_bloom_build_positions", "adl_bloom_get_device", "adl_bloom_set_device",
     "adl_bloom_reload_knobs", "adl_bloom_build_segmented_ex", "adl_bloom_probe_server_launches",
+    "adl_bloom_probe_server_phases",
 )
 
 _LIB = None
@@ -118,6 +119,8 @@ def lib() -> ctypes.CDLL:
         "adl_bloom_set_device": (ctypes.c_int, [i32]),
         "adl_bloom_reload_knobs": (ctypes.c_int, []),
         "adl_bloom_probe_server_launches": (ctypes.c_int, [ctypes.POINTER(u64)]),
+        "adl_bloom_probe_server_phases": (ctypes.c_int, [ctypes.POINTER(u64), ctypes.POINTER(u64),
+                                                          ctypes.POINTER(ctypes.c_double), ctypes.c_int]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

@@ -207,6 +207,7 @@ __global__ __launch_bounds__(256) void fill_maps_kernel(const FilterDesc *__rest
 // workgroup then just takes fewer items.  The counters start at 0 (the host
 // clears them before pass A).  Called by one thread; G % 8 == 0.
 constexpr uint32_t kQueueWords = 256;  // pass A's 8 counters, then pass B's, 64 B apart
+constexpr uint32_t kQueueMinItems = 16;  // items per workgroup below which a pass keeps the static order
 struct GroupQueue {
   uint32_t *q;
   uint32_t G, total, g;
@@ -1570,17 +1571,25 @@ int launch_binned_dt(const Plan &p, Keys keys, uint8_t *d_bitmaps, void *ws, hip
   uint32_t *tab_ws = pos_ws + p.pos_words;
   uint32_t *scr = tab_ws + p.table_words;  // the work-queue counters, pass A's per-wave scratch lines
   uint2 *hp = reinterpret_cast<uint2 *>(scr + p.scratch_words);
-  // While a probe server's kernel is resident (Gets are being served), the
-  // passes take their chunks / tiles from the work queues: a workgroup slowed
-  // or held back by the server's wave on its CU then takes less work instead
-  // of holding up the pass (reads beside builds).  The counters
-  // start at 0.  (Round 5 switched whenever a server object existed, so every
-  // build of a process that had served one Get paid the queues' cost.)
+  // While a probe server's kernel is resident (Gets are being served), a
+  // pass with many items per workgroup takes them from the work queues: a
+  // workgroup slowed or held back by the server's wave on its CU then takes
+  // less work instead of holding up the pass (reads beside
+  // builds).  The counters start at 0.  A pass of a few items per workgroup
+  // keeps the static order: a queue cannot even out less than one item, and
+  // costs its atomics (round 6, profiles/r06/: headline with Gets 0.184 ms
+  // static against 0.203 queued -- 7 chunks and 3 tiles per workgroup;
+  // configs[3] with Gets 4.82 ms static against 3.63 queued -- 180 chunks and
+  // 150 tiles, and pass B's two workgroups per CU leave no room for the
+  // server's wave beside both).  Round 5 queued whenever a server object
+  // existed, so every build of a process that had served one Get paid +12 %.
   const adl_host::Knobs &kn = adl_host::knobs();
   const bool live = kn.build_queues == 3 || (kn.build_queues == 1 && adl_srv::live_servers() > 0) ||
                     (kn.build_queues == 2 && adl_srv::resident_servers() > 0);
-  const bool dyn_a = live && (kn.build_queue_passes & 1) && p.grid_a % 8 == 0;
-  const bool dyn_b = live && (kn.build_queue_passes & 2) && p.grid_b % 8 == 0;
+  const bool many_a = kn.build_queues != 2 || p.total_chunks >= kQueueMinItems * p.grid_a;
+  const bool many_b = kn.build_queues != 2 || p.total_tiles >= kQueueMinItems * p.grid_b || p.occ_b == 2;
+  const bool dyn_a = live && many_a && (kn.build_queue_passes & 1) && p.grid_a % 8 == 0;
+  const bool dyn_b = live && many_b && (kn.build_queue_passes & 2) && p.grid_b % 8 == 0;
   if (dyn_a || dyn_b) ADL_HIP_TRY(hipMemsetAsync(scr, 0, kQueueWords * 4, st));
   FilterTable ft{};
   if constexpr (DT) {

@@ -161,26 +161,35 @@ __device__ __forceinline__ uint32_t ld_sys(const uint32_t *p) {
 
 __device__ __forceinline__ uint64_t now_ticks() { return __builtin_amdgcn_s_memrealtime(); }  // 100 MHz
 
-// A query staged in LDS: 1 iff all k bits of its filter range [b0, b1) are set.
-__device__ __forceinline__ uint32_t serve_query(uint32_t k, uint64_t b0, uint64_t b1, const uint8_t *key,
-                                                uint32_t klen) {
-  k = min(k, 30u);
+// A query staged in LDS, in two phases (timed apart by the kernel): its hash
+// pair and divisor, then the k bit reads of its filter range [b0, b1).
+struct Prep {
+  uint64_t b0;
+  uint32_t k, mbits, h1, h2;
+};
+
+__device__ __forceinline__ Prep prep_query(uint32_t k, uint64_t b0, uint64_t b1, const uint8_t *key, uint32_t klen) {
+  Prep p{b0, min(k, 30u), 0u, 0u, 0u};
   // 0 for an empty range or a filter of 2^31 bits or more (src/filter_block.cpp:50)
-  const uint32_t mbits = b1 > b0 && b1 - b0 <= 0x0fffffffull ? (uint32_t)((b1 - b0) * 8) : 0u;
-  if (!mbits) return 0;
-  uint32_t h1, h2;
-  hash_bytes(key, klen, kSeed1, kSeed2, h1, h2);
-  const FastMod mod = fastmod_for(mbits);
-  const uint8_t *bm = reinterpret_cast<const uint8_t *>(b0);
+  p.mbits = b1 > b0 && b1 - b0 <= 0x0fffffffull ? (uint32_t)((b1 - b0) * 8) : 0u;
+  if (p.mbits) hash_bytes(key, klen, kSeed1, kSeed2, p.h1, p.h2);
+  return p;
+}
+
+// 1 iff all k bits are set (0 for an empty range)
+__device__ __forceinline__ uint32_t read_bits(const Prep &p) {
+  if (!p.mbits) return 0;
+  const FastMod mod = fastmod_for(p.mbits);
+  const uint8_t *bm = reinterpret_cast<const uint8_t *>(p.b0);
   // the answer is the AND of the k bits (src/filter_block.cpp:54-59; the
   // early exit changes no answer): 8 reads in flight at a time
   uint32_t all = 1;
-  for (uint32_t g = 0; g < k; g += 8) {
+  for (uint32_t g = 0; g < p.k; g += 8) {
     uint32_t w[8];
 #pragma unroll
     for (uint32_t u = 0; u < 8; ++u) {
-      const uint32_t p = fastmod(h1 + (g + u < k ? g + u : 0u) * h2, mod);  // past k: bit 0 again
-      w[u] = (uint32_t)(bm[p >> 3] >> (p & 7));
+      const uint32_t q = fastmod(p.h1 + (g + u < p.k ? g + u : 0u) * p.h2, mod);  // past k: bit 0 again
+      w[u] = (uint32_t)(bm[q >> 3] >> (q & 7));
     }
 #pragma unroll
     for (uint32_t u = 0; u < 8; ++u) all &= w[u];
@@ -189,15 +198,15 @@ __device__ __forceinline__ uint32_t serve_query(uint32_t k, uint64_t b0, uint64_
 }
 
 // Query q of a slot staged in LDS.
-__device__ __forceinline__ uint32_t serve_slot_query(const Slot &sl, uint32_t q) {
+__device__ __forceinline__ Prep prep_slot_query(const Slot &sl, uint32_t q) {
   const uint32_t ko = min((uint32_t)sl.koff[q], adl_srv::kMaxKeyBytes);
   const uint32_t ke = min(max((uint32_t)sl.koff[q + 1], ko), adl_srv::kMaxKeyBytes);
-  return serve_query(sl.kq[q], sl.range[2 * q], sl.range[2 * q + 1], sl.keys + ko, ke - ko);
+  return prep_query(sl.kq[q], sl.range[2 * q], sl.range[2 * q + 1], sl.keys + ko, ke - ko);
 }
 
 // The request of a line staged in LDS.
-__device__ __forceinline__ uint32_t serve_line(const Line &ln) {
-  return serve_query(ln.k_klen & 0xFFu, ln.begin, ln.begin + ln.len, ln.key, min(ln.k_klen >> 8, kInlineKeyBytes));
+__device__ __forceinline__ Prep prep_line(const Line &ln) {
+  return prep_query(ln.k_klen & 0xFFu, ln.begin, ln.begin + ln.len, ln.key, min(ln.k_klen >> 8, kInlineKeyBytes));
 }
 
 // One wave.  Lane l polls bell l.  Pending slots are staged kGroup at a time
@@ -208,7 +217,7 @@ __device__ __forceinline__ uint32_t serve_line(const Line &ln) {
 // kLdsReserveWords): a Get does not wait for a build.  amdgpu_num_vgpr(16) is
 // doubled for gfx950's unified register file (as kPassARegs' 60 -> 120): the
 // code object's .vgpr_count is 32.  Unconstrained the kernel would take 63, so
-// 18 VGPRs spill to scratch (72 B per lane): kernel arguments and loop state,
+// 19 VGPRs spill to scratch (76 B per lane, with the phase stamps): kernel arguments and loop state,
 // reloaded once per poll and once per served group, from the L1/L2 the wave
 // alone uses.  tools/kernel_resources.py prints both from the built library
 // and tests/test_kernel_resources.py pins them (no other product kernel on the
@@ -229,7 +238,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(16))) void probe
   const uint64_t t0 = now_ticks();
   uint64_t last = t0, tprev = t0;
   bool closing = false;
-  uint32_t closing_polls = 0;
+  uint32_t closing_polls = 0, idle_polls = 0;
   for (;;) {
     const uint64_t tp = now_ticks();  // this poll (diagnostics: the gap since the previous one)
     const uint32_t bell = ld_sys(&area->bell[lane]);
@@ -255,11 +264,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(16))) void probe
     // (a bounded number of polls: the host writes the line before its bell)
     const bool torn = __ballot(bell != served && !pend) != 0 && (!closing || ++closing_polls < 4096);
     const uint64_t pm = __ballot(pend);
+    const uint64_t t_polled = now_ticks();  // (the poll's loads have returned: pm depends on them)
     if (pm == 0) {
       if (closing && !torn) break;
       const uint64_t t = tp;
       tprev = tp;
-      const bool stop = __ballot(ld_sys(&area->ctl.stop[lane & 15]) != 0) != 0;
+      // the stop word: a second PCIe read after an empty poll, so only every
+      // 8th one (round 5 read it after every empty poll: a poll period of
+      // ~3.1 us instead of ~2; reading it with the bells made every poll
+      // 1.1 us slower, profiles/r06/)
+      const bool stop = (++idle_polls & 7u) == 0 && __ballot(ld_sys(&area->ctl.stop[lane & 15]) != 0) != 0;
       if (stop || t - last > idle_ticks || t - t0 > life_ticks) {
         // Leaving: alive = 0 first, then one more poll, whose bells are
         // served before the wave ends.  A host thread rings its bell and then
@@ -295,14 +309,20 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(16))) void probe
       uint32_t j = kSlots;  // the slot lane 8u + q serves (kSlots: none)
 #pragma unroll
       for (uint32_t x = 0; x < kGroup; ++x) j = u == x ? js[x] : j;
-      uint32_t hit = 0;
+      const uint64_t t_stage = now_ticks();
+      Prep pr{0ull, 0u, 0u, 0u, 0u};
       const uint32_t bj = (uint32_t)__shfl((int)bell, (int)(j < kSlots ? j : 0u));
       if (j < kSlots && (bj & kInlineBit)) {
-        if (q == 0) hit = serve_line(*reinterpret_cast<const Line *>(&lline[16 * (j & (kInlineSlots - 1))]));
+        if (q == 0) pr = prep_line(*reinterpret_cast<const Line *>(&lline[16 * (j & (kInlineSlots - 1))]));
       } else if (j < kSlots) {
         const Slot &sl = *reinterpret_cast<const Slot *>(lslot[u]);
-        if (q < min(sl.n, adl_srv::kMaxQ)) hit = serve_slot_query(sl, q);
+        if (q < min(sl.n, adl_srv::kMaxQ)) pr = prep_slot_query(sl, q);
       }
+      asm volatile("" ::"v"(pr.h1), "v"(pr.h2));  // the hashes are done before the stamp
+      const uint64_t t_hash = now_ticks();
+      const uint32_t hit = read_bits(pr);
+      asm volatile("" ::"v"(hit));  // the bit reads have returned before the stamp
+      const uint64_t t_reads = now_ticks();
       const uint64_t hb = __ballot(hit != 0);
       // lane u < kGroup answers slot js[u]: {seq, (seq << 8) | answer bits} in
       // one 8-byte system-scope store (a plain store can sit in the device's
@@ -316,12 +336,21 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(16))) void probe
         const uint64_t word = (uint64_t)seq | ((uint64_t)((seq << 8) | bits) << 32);
         __hip_atomic_store(reinterpret_cast<uint64_t *>(&area->done[ju]), word, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_SYSTEM);
-        // diagnostics (read by the host under ADL_BLOOM_DEBUG): 10-ns ticks
-        // from the previous poll to the one that found the request, and from
-        // that poll to the answer
-        const uint64_t diag = (uint64_t)(uint32_t)(tp - tprev) | ((uint64_t)(uint32_t)(now_ticks() - tp) << 32);
-        __hip_atomic_store(reinterpret_cast<uint64_t *>(&area->done[ju].pad[0]), diag, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_SYSTEM);
+        // phase stamps (10-ns ticks from the poll that found the request; the
+        // host folds them into adl_bloom_probe_server_phases at the slot's
+        // next request, and prints them for a slow one under ADL_BLOOM_DEBUG):
+        // {seq, gap since the previous poll}, {poll loads back, slot staged},
+        // {hashed, bits read}, {answer stored, seq}, {the poll's start and the
+        // answer's store on the kernel's clock (low 32 bits), the host
+        // relates them to its own clock to place a slow request's delay}
+        const uint64_t ta = now_ticks();
+        uint64_t *dg = reinterpret_cast<uint64_t *>(&area->done[ju].pad[0]);
+        auto w2 = [](uint64_t a, uint64_t b) { return (uint64_t)(uint32_t)a | ((uint64_t)(uint32_t)b << 32); };
+        __hip_atomic_store(dg + 0, w2(seq, tp - tprev), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(dg + 1, w2(t_polled - tp, t_stage - tp), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(dg + 2, w2(t_hash - tp, t_reads - tp), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(dg + 4, w2(tp, ta), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(dg + 3, w2(ta - tp, seq), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       }
       __syncthreads();  // the group's LDS copy is read before the next group overwrites it
     }
@@ -358,6 +387,8 @@ struct Server {
   std::mutex launch_mu;  // launches and gen
   std::mutex slot_mu[kSlots];
   uint32_t seq[kSlots] = {};
+  uint32_t last_bell[kSlots] = {};  // the slot's previous request (its phase stamps are read at the next)
+  uint32_t last_seen[kSlots] = {};  // ... and the host tick at which its answer was seen
   std::atomic<uint32_t> next_slot{0};
   uint64_t id = 0;  // unique per server of this process (a thread's slot is per server)
   uint64_t idle_ticks = 0, life_ticks = 0;
@@ -377,6 +408,61 @@ struct Server {
 namespace {
 
 std::atomic<uint64_t> g_launches{0};
+
+// adl_bloom_probe_server_phases: the kernel's phase stamps of every request
+// whose stamps were read back (ticks of 10 ns), and the host's own time per
+// request (ns)
+struct PhaseStats {
+  std::atomic<uint64_t> requests{0}, stamped{0}, host_ns{0};
+  std::atomic<uint64_t> ticks[6] = {};  // gap, polled, staged, hashed, read, answered
+};
+PhaseStats g_phases;
+
+// The kernel's clock (s_memrealtime, 100 MHz, low 32 bits) against the host's
+// steady clock in the same 10-ns ticks: off = min over requests of (host tick
+// at which an answer was seen - kernel tick at which it was stored), i.e. the
+// clocks' offset plus the fastest answer delivery.  A slow request's bell
+// write and answer are then placed on the kernel's clock (ADL_BLOOM_DEBUG).
+struct ClockCal {
+  std::atomic<uint32_t> ref{0};
+  std::atomic<int32_t> best{INT32_MAX};
+  std::atomic<bool> have{false};
+  void sample(uint32_t host_tick, uint32_t gpu_tick) {
+    const uint32_t d = host_tick - gpu_tick;
+    bool expect = false;
+    if (!have.load(std::memory_order_acquire) && have.compare_exchange_strong(expect, true)) ref.store(d);
+    const int32_t rel = (int32_t)(d - ref.load());
+    int32_t cur = best.load(std::memory_order_relaxed);
+    while (rel < cur && !best.compare_exchange_weak(cur, rel)) {
+    }
+  }
+  bool get(uint32_t *off) const {
+    if (!have.load(std::memory_order_acquire) || best.load() == INT32_MAX) return false;
+    *off = ref.load() + (uint32_t)best.load();
+    return true;
+  }
+};
+ClockCal g_clock;
+
+inline uint32_t host_tick(std::chrono::steady_clock::time_point t) {
+  return (uint32_t)(std::chrono::duration_cast<std::chrono::nanoseconds>(t.time_since_epoch()).count() / 10);
+}
+
+// Fold the stamps of the slot's previous request into g_phases (they were
+// stored after its answer; both copies of its sequence number must match),
+// and its answer's kernel and host times into the clock calibration.
+void fold_phases(const Area *a, uint32_t my, uint32_t bell, uint32_t seen_tick) {
+  if (!bell) return;
+  const uint64_t *dg = reinterpret_cast<const uint64_t *>(&a->done[my].pad[0]);
+  const uint64_t w4 = __atomic_load_n(dg + 4, __ATOMIC_ACQUIRE);
+  const uint64_t w0 = __atomic_load_n(dg + 0, __ATOMIC_ACQUIRE), w1 = __atomic_load_n(dg + 1, __ATOMIC_ACQUIRE);
+  const uint64_t w2 = __atomic_load_n(dg + 2, __ATOMIC_ACQUIRE), w3 = __atomic_load_n(dg + 3, __ATOMIC_ACQUIRE);
+  if ((uint32_t)w0 != bell || (uint32_t)(w3 >> 32) != bell) return;
+  g_clock.sample(seen_tick, (uint32_t)(w4 >> 32));
+  const uint64_t v[6] = {w0 >> 32, (uint32_t)w1, w1 >> 32, (uint32_t)w2, w2 >> 32, (uint32_t)w3};
+  for (int i = 0; i < 6; ++i) g_phases.ticks[i].fetch_add(v[i], std::memory_order_relaxed);
+  g_phases.stamped.fetch_add(1, std::memory_order_relaxed);
+}
 
 void set_stop(Server *s, uint32_t v) {
   for (uint32_t &w : s->host->ctl.stop) __atomic_store_n(&w, v, __ATOMIC_SEQ_CST);
@@ -399,13 +485,45 @@ void stop_launcher(Server *s) {
   if (s->launcher.joinable()) s->launcher.join();
 }
 
+// Stop a server whose launcher thread has been joined (no launch can start):
+// raise stop, then wait -- on the mapped control words alone, no runtime call
+// -- until the last launched generation has published gen_done.  A successor
+// queued behind the running kernel (Server::launcher) has then started, seen
+// stop at its first poll and left too, so no dispatch of the server's stream
+// is pending when its completion events are waited for and the stream is
+// torn down (a process that exited with a successor queued is
+// the state the CU-masked stream's exit hang left unexplained).  With
+// ADL_BLOOM_DEBUG the state found and the wait are logged.
+void stop_and_drain(Server *s, const char *why) {
+  const uint32_t started0 = __atomic_load_n(&s->host->ctl.gen_started, __ATOMIC_SEQ_CST);
+  const uint32_t done0 = __atomic_load_n(&s->host->ctl.gen_done, __ATOMIC_SEQ_CST);
+  const uint32_t alive0 = __atomic_load_n(&s->host->ctl.alive, __ATOMIC_SEQ_CST);
+  set_stop(s, 1);
+  const auto t0 = std::chrono::steady_clock::now();
+  bool drained = !s->launched;
+  while (!drained && std::chrono::steady_clock::now() - t0 < std::chrono::seconds(2)) {
+    drained = __atomic_load_n(&s->host->ctl.gen_done, __ATOMIC_ACQUIRE) == s->gen;
+    if (!drained) __builtin_ia32_pause();
+  }
+  if (s->debug)
+    fprintf(stderr,
+            "adl_bloom server %s: launched generation %u, started %u, done %u, alive %u (%s); "
+            "%s after %.1f us\n",
+            why, s->gen, started0, done0, alive0,
+            !s->launched ? "never launched"
+            : started0 != s->gen ? "a successor queued, not started"
+            : done0 != s->gen ? "running" : "exited",
+            drained ? "drained" : "NOT drained (the runtime's completion events decide)",
+            std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
+  wait_all(s);
+}
+
 void stop_all_at_exit() {
   std::lock_guard<std::mutex> g(g_reg_mu);
   if (!g_reg) return;
   for (Server *s : *g_reg) {
     stop_launcher(s);
-    set_stop(s, 1);
-    wait_all(s);
+    stop_and_drain(s, "at exit");
   }
 }
 
@@ -580,8 +698,7 @@ void destroy(Server *s) {
       }
   }
   stop_launcher(s);
-  set_stop(s, 1);
-  wait_all(s);
+  stop_and_drain(s, "destroy");
   (void)hipStreamSynchronize(s->stream);
   for (hipEvent_t e : s->exited) (void)hipEventDestroy(e);
   (void)hipStreamDestroy(s->stream);
@@ -620,6 +737,7 @@ int probe(Server *s, const uint8_t *h_keys, const uint64_t *h_offsets, uint32_t 
     my_server = s->id;
   }
   std::lock_guard<std::mutex> slot_guard(s->slot_mu[my]);
+  fold_phases(s->host, my, s->last_bell[my], s->last_seen[my]);
   // 31-bit sequence numbers, never 0 (the initial done); bit 31 of the bell
   // value says where the request is
   s->seq[my] = (s->seq[my] + 1) & ~kInlineBit;
@@ -627,6 +745,8 @@ int probe(Server *s, const uint8_t *h_keys, const uint64_t *h_offsets, uint32_t 
   const bool inl = my < kInlineSlots && n == 1 && key_bytes <= kInlineKeyBytes && range[1] >= range[0] &&
                    range[1] - range[0] <= 0xFFFFFFFFull;
   const uint32_t seq = s->seq[my] | (inl ? kInlineBit : 0u);
+  s->last_bell[my] = seq;
+  const auto tw0 = std::chrono::steady_clock::now();
   const uint8_t *kp = h_keys + (h_offsets ? h_offsets[0] : 0);
   if (inl) {
     // the whole line, check word last computed, in one copy; then the bell
@@ -700,12 +820,28 @@ int probe(Server *s, const uint8_t *h_keys, const uint64_t *h_offsets, uint32_t 
       // the kernel's own view, stored after the answer: wait for it briefly
       const auto tw = std::chrono::steady_clock::now();
       while (std::chrono::steady_clock::now() - tw < std::chrono::microseconds(50)) __builtin_ia32_pause();
-      const uint64_t diag = __atomic_load_n(reinterpret_cast<const uint64_t *>(&s->host->done[my].pad[0]), __ATOMIC_ACQUIRE);
+      const uint64_t *dg = reinterpret_cast<const uint64_t *>(&s->host->done[my].pad[0]);
+      const uint64_t w0 = __atomic_load_n(dg + 0, __ATOMIC_ACQUIRE), w1 = __atomic_load_n(dg + 1, __ATOMIC_ACQUIRE);
+      const uint64_t w2 = __atomic_load_n(dg + 2, __ATOMIC_ACQUIRE), w3 = __atomic_load_n(dg + 3, __ATOMIC_ACQUIRE);
+      const uint64_t w4 = __atomic_load_n(dg + 4, __ATOMIC_ACQUIRE);
+      // on the kernel's clock: when the bell was written, when the poll that
+      // found it started, and how much later than the fastest delivery the
+      // answer reached this thread
+      uint32_t off = 0;
+      if (g_clock.get(&off))
+        fprintf(stderr,
+                "adl_bloom server: slow request on the kernel's clock: the poll that found it started %.2f us after "
+                "the bell was written; the answer reached the host %.2f us later than the fastest answer does\n",
+                (double)(int32_t)((uint32_t)w4 + off - host_tick(tb)) / 100.0,
+                (double)(int32_t)(host_tick(t1) - ((uint32_t)(w4 >> 32) + off)) / 100.0);
       fprintf(stderr,
               "adl_bloom server: slow request %.1f us (alive check / relaunch %.1f us%s, answer wait %.1f us; "
-              "kernel: %.2f us since its previous poll, %.2f us to answer)\n",
-              us_ring + us_wait, us_ring, relaunched ? ", relaunched" : "", us_wait, (double)(uint32_t)diag / 100.0,
-              (double)(uint32_t)(diag >> 32) / 100.0);
+              "kernel%s: %.2f us since its previous poll; from the poll that found it: loads back %.2f, "
+              "staged %.2f, hashed %.2f, bits read %.2f, answered %.2f us)\n",
+              us_ring + us_wait, us_ring, relaunched ? ", relaunched" : "", us_wait,
+              (uint32_t)w0 == seq && (uint32_t)(w3 >> 32) == seq ? "" : " (stamps of another request)",
+              (double)(w0 >> 32) / 100.0, (double)(uint32_t)w1 / 100.0, (double)(w1 >> 32) / 100.0,
+              (double)(uint32_t)w2 / 100.0, (double)(w2 >> 32) / 100.0, (double)(uint32_t)w3 / 100.0);
     }
   }
   // no successor queued behind the running kernel (the last launched one has
@@ -719,11 +855,34 @@ int probe(Server *s, const uint8_t *h_keys, const uint64_t *h_offsets, uint32_t 
     }
     s->lcv.notify_one();
   }
+  s->last_seen[my] = host_tick(std::chrono::steady_clock::now());
+  g_phases.requests.fetch_add(1, std::memory_order_relaxed);
+  g_phases.host_ns.fetch_add(
+      (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - tw0).count(),
+      std::memory_order_relaxed);
   for (uint64_t q = 0; q < n; ++q) h_out[q] = (uint8_t)((bits >> q) & 1u);
   return ADL_OK;
 }
 
 }  // namespace adl_srv
+
+extern "C" int adl_bloom_probe_server_phases(uint64_t *requests, uint64_t *stamped, double *avg_us, int reset) {
+  using adl_srv::g_phases;
+  const uint64_t n = g_phases.requests.load(), ns = g_phases.stamped.load();
+  if (requests) *requests = n;
+  if (stamped) *stamped = ns;
+  if (avg_us) {
+    for (int i = 0; i < 6; ++i) avg_us[i] = ns ? (double)g_phases.ticks[i].load() / 100.0 / (double)ns : 0.0;
+    avg_us[6] = n ? (double)g_phases.host_ns.load() / 1000.0 / (double)n : 0.0;
+  }
+  if (reset) {
+    g_phases.requests = 0;
+    g_phases.stamped = 0;
+    g_phases.host_ns = 0;
+    for (auto &t : g_phases.ticks) t = 0;
+  }
+  return ADL_OK;
+}
 
 extern "C" int adl_bloom_probe_server_launches(uint64_t *launches) {
   if (!launches) return ADL_ERR_INVALID_ARG;

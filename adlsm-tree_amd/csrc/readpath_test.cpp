@@ -31,6 +31,12 @@
 //   readpath_test --coexist [reps]
 //     Single-key Gets while the headline build and a configs[3]-shaped build
 //     run on another thread (Coexist below).
+//
+//   readpath_test --exit-queued
+//     Serves Gets until the probe server has a successor kernel queued behind
+//     the running one, then returns from main with both still on the
+//     server's stream: the process must exit (the atexit stop path drains the
+//     queued successor; ADL_BLOOM_DEBUG=1 logs the state it found).
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -236,6 +242,7 @@ int Tails(size_t calls) {
   for (size_t i = 0; i < q.size(); ++i) want[i] = reader.IsKeyExists(0, q[i]);
   uint64_t l0 = 0, l1 = 0;
   if (adl_bloom_probe_server_launches(&l0)) return 1;
+  (void)adl_bloom_probe_server_phases(nullptr, nullptr, nullptr, 1);
   std::vector<double> lat, lat_relaunch, lat_plain, lat_switched;
   lat.reserve(calls);
   size_t bad = 0;
@@ -260,6 +267,9 @@ int Tails(size_t calls) {
   }
   const double elapsed = Now() - t_start;
   if (adl_bloom_probe_server_launches(&l1)) return 1;
+  uint64_t ph_req = 0, ph_st = 0;
+  double ph[7] = {};
+  (void)adl_bloom_probe_server_phases(&ph_req, &ph_st, ph, 0);
   // host-only control: spins of the median call's length, timed the same way
   const double spin_us = Pct(lat, 0.5);
   std::vector<double> ctl;
@@ -291,7 +301,11 @@ int Tails(size_t calls) {
   printf(", \"over_30us\": %zu, \"over_30us_not_switched_out\": %zu, \"control_over_30us\": %zu, \"top_us\": [",
          over(lat, 30.0), over(lat_plain, 30.0) + over(lat_relaunch, 30.0), over(ctl, 30.0));
   for (size_t i = 0; i < top.size(); ++i) printf("%s%.1f", i ? ", " : "", top[i]);
-  printf("], \"elapsed_s\": %.3f, \"server_launches\": %llu, \"mismatches\": %zu}\n", elapsed,
+  printf("], \"server_phases_us\": {\"requests\": %llu, \"stamped\": %llu, \"gap_since_previous_poll\": %.3f, "
+         "\"poll_loads_back\": %.3f, \"slot_staged\": %.3f, \"hashed\": %.3f, \"bits_read\": %.3f, "
+         "\"answer_stored\": %.3f, \"host_per_request\": %.3f}",
+         (unsigned long long)ph_req, (unsigned long long)ph_st, ph[0], ph[1], ph[2], ph[3], ph[4], ph[5], ph[6]);
+  printf(", \"elapsed_s\": %.3f, \"server_launches\": %llu, \"mismatches\": %zu}\n", elapsed,
          (unsigned long long)(l1 - l0), bad);
   fflush(stdout);
   fprintf(stderr, "tails: printed, tearing down\n");
@@ -452,6 +466,33 @@ int Coexist(int reps) {
   return bad ? 1 : 0;
 }
 
+// Exit with a successor queued.  The cache and reader are
+// leaked on purpose: no destructor runs before exit, so the atexit stop path
+// alone must drain the server's stream.
+int ExitQueued() {
+  RC rc;
+  Level lv = BuildLevel(1, 50000, 200000, &rc);
+  if (rc) return 1;
+  auto *cache = new FilterCache(1ull << 26, 8, kBpk);
+  auto *reader = new FilterBlockReader;
+  if (cache->status() || cache->Put(lv.tables[0].oid, lv.blocks[0]) ||
+      reader->Init(lv.blocks[0], *cache, lv.tables[0].oid))
+    return 1;
+  const std::vector<std::string> q = Queries(64, 200000, 3);
+  uint64_t l0 = 0, l = 0;
+  (void)adl_bloom_probe_server_launches(&l0);
+  // the first Get launches the server; a later one asks the launcher thread
+  // for a successor, which it queues behind the running kernel (1 s life)
+  for (int i = 0; i < 2000 && l - l0 < 2; ++i) {
+    (void)reader->IsKeyExists(0, q[i % q.size()]);
+    std::this_thread::sleep_for(std::chrono::microseconds(20));
+    (void)adl_bloom_probe_server_launches(&l);
+  }
+  printf("{\"server_launches\": %llu, \"exiting\": true}\n", (unsigned long long)(l - l0));
+  fflush(stdout);
+  return l - l0 >= 2 ? 0 : 3;
+}
+
 }  // namespace
 
 int main(int argc, char **argv) {
@@ -462,6 +503,7 @@ int main(int argc, char **argv) {
     return rc;
   }
   if (argc > 1 && strcmp(argv[1], "--coexist") == 0) return Coexist(argc > 2 ? atoi(argv[2]) : 5);
+  if (argc > 1 && strcmp(argv[1], "--exit-queued") == 0) return ExitQueued();
   if (argc < 2) {
     fprintf(stderr, "usage: readpath_test <outdir> [threads] [rounds] | --bench\n");
     return 2;

@@ -368,6 +368,15 @@ int adl_bloom_reload_knobs(void);
  * tests (readpath_test --tails). */
 int adl_bloom_probe_server_launches(uint64_t *launches);
 
+/* (instrumentation) The resident probe server's request phases, averaged over
+ * the requests since the last reset: *requests served, *stamped of them with
+ * the kernel's stamps read back, and avg_us[7] = the kernel's gap since its
+ * previous poll, then from the poll that found the request: its loads back,
+ * the slot staged in LDS, the hashes done, the bit reads back, the answer
+ * stored; avg_us[6] = the host's time per request (the request written to the
+ * answer read).  reset != 0 clears the counters after reading them. */
+int adl_bloom_probe_server_phases(uint64_t *requests, uint64_t *stamped, double *avg_us, int reset);
+
 /* ---------------------------------------------------------------- synthetic data */
 
 /* SURVEY.md §8d SplitMix64 16-byte keys, generated on the device: key i of the

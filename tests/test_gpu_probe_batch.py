@@ -271,3 +271,29 @@ def test_probe_batch_hot_filter_split(dev, ab, oracle, hot_bytes, F):
     keys = rng.integers(0, 256, (n, 16), dtype=np.uint8)
     got = _check(dev, ab, oracle, arena, off, keys, fid, bpk=10)
     assert not got[fid >= F].any()
+
+
+def test_probe_batch_filter_spread_over_many_blocks(dev, ab, oracle):
+    """A filter with about one query per bucketing block of 8 192, over more
+    than 4 096 blocks (36 M queries): its chunk's hashes are gathered from more
+    blocks than pb_bin's LDS block list holds, so the chunk's queries find
+    their blocks by a search in global memory.  Every answer equals the direct
+    kernel's, and the thin filter's equal the oracle's."""
+    sizes = [200_000, 50_000]
+    arena, off = _arena(oracle, sizes, seed0=5150)
+    n = 4100 * 8192 + 777
+    fid = np.zeros(n, np.uint32)
+    thin = np.arange(5, n, 8192)
+    fid[thin] = 1
+    keys = oracle.splitmix_keys16(515, n)
+    member = oracle.splitmix_keys16(5151, sizes[1])
+    keys[thin[::2]] = member[np.arange(thin[::2].size) % sizes[1]]
+    d = lambda a: dev.from_numpy(a).cuda()  # noqa: E731
+    d_keys, d_fid, d_arena, d_off = d(keys), d(fid.view(np.int32)), d(arena), d(off.view(np.int64))
+    got = ab.probe_batch(d_keys, d_fid, d_arena, d_off).cpu().numpy()
+    direct = ab.probe_multi(d_keys, d_fid, d_arena, d_off).cpu().numpy()
+    bad = np.nonzero(got != direct)[0]
+    assert bad.size == 0, f"{bad.size} answers differ, first at {bad[:5]}"
+    want = oracle.probe_multi(keys[thin], fid[thin], arena, off)
+    assert np.array_equal(got[thin], want)
+    assert got[thin[::2]].all()

@@ -499,3 +499,19 @@ def test_probe_server_tails(dev):
     assert d["mismatches"] == 0
     assert d["single_key_us"]["calls"] == 20000
     assert d["server_launches"] >= 10
+
+
+def test_probe_server_exit_with_queued_successor(dev):
+    """A process that returns from main while the server has a successor
+    kernel queued behind the running one exits promptly: the atexit stop path
+    waits on the mapped control words until the queued successor has started,
+    seen stop and left, before the runtime's teardown (VERDICT r5 #8)."""
+    exe = os.path.join(ROOT, "adlsm-tree_amd", "bin", "readpath_test")
+    t0 = time.perf_counter()
+    r = subprocess.run([exe, "--exit-queued"], capture_output=True, text=True, timeout=60,
+                       env=dict(os.environ, ADL_BLOOM_DEBUG="1"))
+    print(r.stdout, r.stderr[-2000:])
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert time.perf_counter() - t0 < 30
+    line = [x for x in r.stderr.splitlines() if "adl_bloom server at exit" in x]
+    assert line and "drained" in line[-1] and "NOT drained" not in line[-1], r.stderr[-2000:]

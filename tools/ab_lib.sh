@@ -7,7 +7,7 @@ mkdir -p gpurun_out
 IFS='|' read -ra VARIANTS <<< "${LIBS}"
 for rep in $(seq 1 ${REPS:-3}); do
   for v in "${VARIANTS[@]}"; do
-    out=$(ADL_BLOOM_LIB=$v timeout -k 10 300 python3 bench.py --steps ${STEPS:-30} --warmup 5 --no-cpu-baseline --no-e2e ${BENCH_ARGS:-} 2>/dev/null | grep '^{')
+    out=$(ADL_BLOOM_LIB=$v timeout -k 10 300 python3 bench.py --steps ${STEPS:-30} --warmup 5 --no-cpu-baseline --no-e2e --no-sub-records --no-reader ${BENCH_ARGS:-} 2>/dev/null | grep '^{')
     rc=$?
     [ $rc -ne 0 ] && { echo "variant '$v' rc=$rc"; exit $rc; }
     echo "$v :: $(echo "$out" | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"], d["roofline"]["us_per_step"], d["parity"])')"

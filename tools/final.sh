@@ -33,7 +33,7 @@ bash tools/bench_all.sh || exit 1
 cp gpurun_out/bench_all.jsonl "$OUT/bench_all.jsonl"
 step rocprof
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
-  python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-e2e --no-compaction-strong > "$OUT/prof_bench.json" 2> "$OUT/prof.err" || exit 1
+  python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-e2e --no-compaction-strong --no-sub-records --no-reader > "$OUT/prof_bench.json" 2> "$OUT/prof.err" || exit 1
 step rocprof_varlen
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_varlen" -o run --output-format csv -- \
   python3 bench.py --steps 20 --warmup 5 --workload varlen --no-cpu-baseline --no-e2e > "$OUT/prof_varlen_bench.json" 2> "$OUT/prof_varlen.err" || exit 1

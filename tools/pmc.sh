@@ -8,7 +8,7 @@ cd "$(dirname "$0")/.."
 OUT=${OUT:-gpurun_out/pmc}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-CMD=(python3 bench.py --steps ${PMC_STEPS:-4} --warmup 1 --no-cpu-baseline --no-e2e --no-compaction-strong ${BENCH_ARGS:-})
+CMD=(python3 bench.py --steps ${PMC_STEPS:-4} --warmup 1 --no-cpu-baseline --no-e2e --no-compaction-strong --no-sub-records --no-reader ${BENCH_ARGS:-})
 [ "${LIST:-0}" = 1 ] && { timeout -k 10 120 rocprofv3 -L > "$OUT/counters.txt" 2>&1; echo "list rc=$?"; }
 i=0
 while IFS= read -r group; do
