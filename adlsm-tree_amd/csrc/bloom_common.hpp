@@ -208,6 +208,7 @@ struct Knobs {
   // ADL_BLOOM_BUILD_QUEUE_PASSES: which passes (bit 0 pass A, bit 1 pass B).
   uint32_t build_queues = 2;
   uint32_t build_queue_passes = 3;
+  bool server_invalidate = false;  // ADL_BLOOM_SERVER_INVALIDATE: the server invalidates its caches at every request
   bool debug = false;             // ADL_BLOOM_DEBUG: the plan and failing HIP calls to stderr
   uint32_t exp = 0, pb_exp = 0;   // ADL_BLOOM_EXP / ADL_PB_EXP: diagnostics build (make stamps) only
 
@@ -228,6 +229,7 @@ struct Knobs {
     pipe_mb = u64("ADL_BLOOM_PIPE_MB", 128);
     build_queues = (uint32_t)u64("ADL_BLOOM_BUILD_QUEUES", 2);
     build_queue_passes = (uint32_t)u64("ADL_BLOOM_BUILD_QUEUE_PASSES", 3);
+    server_invalidate = u64("ADL_BLOOM_SERVER_INVALIDATE", 0) != 0;
     debug = u64("ADL_BLOOM_DEBUG", 0) != 0;
 #ifdef ADL_BLOOM_STAMPS
     exp = (uint32_t)u64("ADL_BLOOM_EXP", 0);

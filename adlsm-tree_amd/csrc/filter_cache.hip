@@ -119,6 +119,9 @@ struct adl_bloom_filter_cache {
   // adl_srv::kTimeout), small batches go straight to a launch until this
   // steady-clock time (ns), instead of each waiting out the timeout again
   std::atomic<int64_t> srv_backoff_until{0};
+  // published puts so far (the server invalidates its caches before it reads
+  // bits of a range that may have been written since it last did)
+  std::atomic<uint64_t> epoch{1};
 
   bool alloc(uint64_t size, uint64_t &at) {
     for (auto it = free_.begin(); it != free_.end(); ++it) {
@@ -265,6 +268,7 @@ int adl_bloom_filter_cache_put(adl_bloom_filter_cache *c, const char *oid, uint6
     mine->state = adl_bloom_filter_cache::kLive;
     c->lru.splice(c->lru.begin(), c->limbo, mine);
     c->index[key] = c->lru.begin();
+    c->epoch.fetch_add(1, std::memory_order_release);  // (under the lock: before any probe can resolve it)
     while (c->lru.size() > c->max_tables) c->retire(std::prev(c->lru.end()));
     c->freed.notify_all();  // a put waiting for room may evict this entry now
     return ADL_OK;
@@ -380,7 +384,8 @@ int adl_bloom_filter_cache_probe(adl_bloom_filter_cache *c, const char *const *o
           rng[2 * i + 1] = a0 + be[num_tables + h_table[i]];
           kq[i] = kt[h_table[i]];
         }
-        int rc = adl_srv::probe(srv, h_keys, h_offsets, key_stride, n, rng, kq, h_out);
+        int rc = adl_srv::probe(srv, h_keys, h_offsets, key_stride, n, rng, kq,
+                                c->epoch.load(std::memory_order_acquire), h_out);
         if (rc == ADL_OK && adl_host::g_test_faults.take(ADL_TEST_FAULT_CACHE_COMPLETION) >= 0) rc = ADL_ERR_DEVICE;
         // kBusy: no answer in adl_srv::kTimeout (a healthy GPU with no room for
         // the server's wave): probe by a launch below, the ranges still pinned

@@ -109,7 +109,7 @@ Plan make_plan(uint64_t n, uint32_t F, int32_t bpk) {
   p.o_start = take((uint64_t)(F + 1) * p.nb * 4);
   p.ng = (p.nb + kScanGroup - 1) / kScanGroup;
   p.o_gsum = take((uint64_t)(F + 1) * p.ng * 4);
-  p.o_cf = take(p.maxch * 16);
+  p.o_cf = take(p.maxch * 4);
   p.o_dest = take(n * 2);
   p.o_hs = take(n * 8);
   p.o_ent = take(p.maxch * p.k * p.C * 4);
@@ -224,7 +224,7 @@ constexpr uint64_t kTileWork = kTileBytes / 4;
 
 __global__ __launch_bounds__(kBlk) void pb_plan_kernel(uint32_t *__restrict__ gsum, uint32_t ng, uint32_t F,
                                                        uint32_t C, uint64_t maxch, PFilter *__restrict__ desc,
-                                                       uint4 *__restrict__ chunk_rec,
+                                                       uint32_t *__restrict__ chunk_filter,
                                                        uint32_t *__restrict__ scal, uint32_t k, uint32_t G,
                                                        uint32_t *__restrict__ split) {
   __shared__ uint32_t scratch[kBlk / kWave + 1];
@@ -280,10 +280,7 @@ __global__ __launch_bounds__(kBlk) void pb_plan_kernel(uint32_t *__restrict__ gs
       desc[f].chunk_base = (uint32_t)(cc + pc);
       desc[f].nchunks = nc;
       desc[f].table_base = ct + before + incl - te;
-      // per chunk {filter, first slot in filter order, queries, index in the
-      // filter}: pb_bin reads one record per chunk, two chunks ahead
-      for (uint32_t j = 0; j < nc; ++j)
-        chunk_rec[cc + pc + j] = make_uint4(f, (uint32_t)(cq + pq) + j * C, min(C, tot - j * C), j);
+      for (uint32_t j = 0; j < nc; ++j) chunk_filter[cc + pc + j] = f;
       if (f == F) scal[1] = (uint32_t)(cc + pc);  // chunks over all filters
     }
     cq += all_q;
@@ -291,7 +288,7 @@ __global__ __launch_bounds__(kBlk) void pb_plan_kernel(uint32_t *__restrict__ gs
     ct += all_t;
   }
   __syncthreads();
-  for (uint64_t j = cc + threadIdx.x; j < maxch; j += kBlk) chunk_rec[j] = make_uint4(kSentinel, 0, 0, 0);
+  for (uint64_t j = cc + threadIdx.x; j < maxch; j += kBlk) chunk_filter[j] = kSentinel;
   // the work before tile t of filter f (filters in order, a filter's queries
   // spread evenly over its tiles)
   auto work = [&](uint32_t f, uint32_t t) -> uint64_t {
@@ -426,14 +423,10 @@ __global__ __launch_bounds__(kBlk) void pb_scatter_kernel(const uint4 *__restric
 // All k bits of every query are binned in one round (the reference stops at
 // the first clear bit, src/filter_block.cpp:54-59; the answer is the AND
 // either way, and a two-round form measured slower: HISTORY.md).  KFIX = 0:
-// runtime k.  A chunk's record (filter, first slot, queries, index) is
-// loaded two chunks ahead and its hashes one chunk ahead, so no dependent
-// load chain stands between one chunk and the next (round 5 looked up the
-// next chunk's filter and then its descriptor before its hash loads could
-// issue: two scalar round trips per chunk).
+// runtime k.
 template <int KFIX>
 __global__ __launch_bounds__(kBlk) void pb_bin_kernel(const uint2 *__restrict__ hs, const PFilter *__restrict__ desc,
-                                                      const uint4 *__restrict__ chunk_rec,
+                                                      const uint32_t *__restrict__ chunk_filter,
                                                       const uint32_t *__restrict__ scal, uint32_t k, uint32_t C,
                                                       uint32_t *__restrict__ ent, uint32_t *__restrict__ table,
                                                       uint8_t *__restrict__ res, uint32_t exp) {
@@ -451,30 +444,28 @@ __global__ __launch_bounds__(kBlk) void pb_bin_kernel(const uint2 *__restrict__ 
   const uint32_t G = gridDim.x;
   // answers are one "cleared" bit per slot (1: a tested bit was clear, the answer is 0)
   uint32_t *clrw = reinterpret_cast<uint32_t *>(res);
-  // {filter, first slot in filter order, queries, index in the filter}
-  auto rec = [&](uint32_t c) { return c < total_chunks ? chunk_rec[c] : make_uint4(kSentinel, 0u, 1u, 0u); };
-  auto fetch = [&](const uint4 &rc, uint2 (&h)[kCPT]) {
-    if (rc.x == kSentinel) return;
+  auto fetch = [&](uint32_t c, uint2 (&h)[kCPT]) {
+    if (c >= total_chunks) return;
+    const uint32_t f = chunk_filter[c];
+    const uint32_t j = c - desc[f].chunk_base;
+    const uint32_t q0 = desc[f].qbase + j * C;
+    const uint32_t cnt = min(C, desc[f].cnt - j * C);
 #pragma unroll
-    for (uint32_t r = 0; r < kCPT; ++r) h[r] = hs[rc.y + min(tid + r * kBlk, rc.z - 1u)];
+    for (uint32_t r = 0; r < kCPT; ++r) h[r] = hs[q0 + min(tid + r * kBlk, cnt - 1u)];
   };
-  uint4 rn = rec(blockIdx.x), rn1 = rec(blockIdx.x + G);
   uint2 nxt[kCPT];
-  fetch(rn, nxt);
+  fetch(blockIdx.x, nxt);
   for (uint32_t c = blockIdx.x; c < total_chunks; c += G) {
-    const uint4 rcur = rn;  // this chunk
-    rn = rn1;               // chunk c + G: its hashes load now
-    rn1 = rec(c + 2 * G);   // chunk c + 2G: its record loads now
     uint2 cur[kCPT];
     bool live[kCPT];
 #pragma unroll
     for (uint32_t r = 0; r < kCPT; ++r) cur[r] = nxt[r], live[r] = true;
-    fetch(rn, nxt);
-    const uint32_t f = rcur.x;
+    fetch(c + G, nxt);
+    const uint32_t f = chunk_filter[c];
     const PFilter d = desc[f];
-    const uint32_t j = rcur.w;
-    const uint32_t q0 = rcur.y;
-    const uint32_t cnt = rcur.z;
+    const uint32_t j = c - d.chunk_base;
+    const uint32_t q0 = d.qbase + j * C;
+    const uint32_t cnt = min(C, d.cnt - j * C);
     const uint32_t T = d.tiles;
     const FastMod mod{d.m, d.magic, d.shift, 0u};
     __syncthreads();  // the previous chunk's entries are read out of lpos
@@ -980,7 +971,7 @@ int adl_bloom_probe_batch_device(const uint8_t *d_keys, const uint64_t *d_offset
   uint32_t *scal = reinterpret_cast<uint32_t *>(ws + p.o_scal);
   uint32_t *cnt = reinterpret_cast<uint32_t *>(ws + p.o_cnt);
   uint32_t *start = reinterpret_cast<uint32_t *>(ws + p.o_start);
-  uint4 *cf = reinterpret_cast<uint4 *>(ws + p.o_cf);
+  uint32_t *cf = reinterpret_cast<uint32_t *>(ws + p.o_cf);
   uint16_t *dest = reinterpret_cast<uint16_t *>(ws + p.o_dest);
   uint2 *hs = reinterpret_cast<uint2 *>(ws + p.o_hs);
   uint32_t *ent = reinterpret_cast<uint32_t *>(ws + p.o_ent);

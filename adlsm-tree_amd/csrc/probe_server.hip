@@ -61,6 +61,7 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
@@ -83,6 +84,14 @@ constexpr uint32_t kHdrBytes = 16;   // seq (unused by the device), n, (unused),
 constexpr uint32_t kInlineSlots = 4;       // slots whose one-query requests can sit in their bell line
 constexpr uint32_t kInlineKeyBytes = 40;
 constexpr uint32_t kInlineBit = 0x80000000u;  // in a bell: the request is in the slot's line
+// In a bell: the cache arena changed since the server last dropped its
+// cached copies of it (a put published a block): the wave invalidates its
+// caches (a system-scope acquire) before it reads any filter bits of that
+// poll.  Round 5 did so after every poll that found a request, which dropped
+// the L2 of the server's XCD under a co-running build ~100 000 times a second
+// (pass B 10 % slower beside Gets, profiles/r06/).
+constexpr uint32_t kInvalidateBit = 0x40000000u;
+constexpr uint32_t kSeqMask = 0x3FFFFFFFu;
 constexpr uint32_t kLineCheck = 0x5EED5EEDu;  // the XOR of line_word_hash over a line's 16 words
 constexpr uint32_t kRangeOff = kHdrBytes;                      // u64 begin, end per query
 constexpr uint32_t kKoffOff = kRangeOff + 16 * adl_srv::kMaxQ;  // u16 offsets, kMaxQ + 1
@@ -239,6 +248,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(16))) void probe
   uint64_t last = t0, tprev = t0;
   bool closing = false;
   uint32_t closing_polls = 0, idle_polls = 0;
+  // (Two polls in flight -- poll i + 2 issued before poll i is examined --
+  // would halve the wait for a bell, but the wave has no registers for them:
+  // the compiler spilled the in-flight values and waited for each load before
+  // its spill store, serialising the polls again.)
   for (;;) {
     const uint64_t tp = now_ticks();  // this poll (diagnostics: the gap since the previous one)
     const uint32_t bell = ld_sys(&area->bell[lane]);
@@ -265,16 +278,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(16))) void probe
     const bool torn = __ballot(bell != served && !pend) != 0 && (!closing || ++closing_polls < 4096);
     const uint64_t pm = __ballot(pend);
     const uint64_t t_polled = now_ticks();  // (the poll's loads have returned: pm depends on them)
+    const bool last_poll = closing;  // a poll issued after alive was cleared
     if (pm == 0) {
-      if (closing && !torn) break;
+      if (last_poll && !torn) break;
       const uint64_t t = tp;
       tprev = tp;
       // the stop word: a second PCIe read after an empty poll, so only every
       // 8th one (round 5 read it after every empty poll: a poll period of
       // ~3.1 us instead of ~2; reading it with the bells made every poll
       // 1.1 us slower, profiles/r06/)
-      const bool stop = (++idle_polls & 7u) == 0 && __ballot(ld_sys(&area->ctl.stop[lane & 15]) != 0) != 0;
-      if (stop || t - last > idle_ticks || t - t0 > life_ticks) {
+      const bool stop = !closing && (++idle_polls & 7u) == 0 && __ballot(ld_sys(&area->ctl.stop[lane & 15]) != 0) != 0;
+      if (!closing && (stop || t - last > idle_ticks || t - t0 > life_ticks)) {
         // Leaving: alive = 0 first, then one more poll, whose bells are
         // served before the wave ends.  A host thread rings its bell and then
         // reads alive (both sequentially consistent): if it read 1, this
@@ -288,7 +302,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(16))) void probe
       __builtin_amdgcn_s_sleep(1);
       continue;
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // the slots were written before their bells
+    // (the slots and their keys are read below with system-scope loads issued
+    // after this poll's bells came back, so they are at least as new as the
+    // bells; only the arena's bits can be stale in this wave's caches)
+    if (__ballot(pend && (bell & kInvalidateBit)) != 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
     for (uint64_t m = pm; m;) {
       uint32_t js[kGroup];
       uint64_t v[kGroup];
@@ -357,7 +374,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(16))) void probe
     if (pend) served = bell;
     last = now_ticks();
     tprev = tp;
-    if (closing && !torn) break;
+    if (last_poll && !torn) break;
   }
   // the last poll's answers are out: the host may launch the next kernel (on
   // the other stream) as soon as it sees this
@@ -393,6 +410,11 @@ struct Server {
   uint64_t id = 0;  // unique per server of this process (a thread's slot is per server)
   uint64_t idle_ticks = 0, life_ticks = 0;
   bool debug = false;  // ADL_BLOOM_DEBUG at creation (the launcher thread must not read knobs() while a reload runs)
+  bool invalidate_always = false;  // ADL_BLOOM_SERVER_INVALIDATE=1 at creation
+  // the cache arena's epoch (bumped by each published put) up to which the
+  // running wave has invalidated its caches; a new kernel starts with clean
+  // caches, so a launch counts too (ensure_running)
+  std::atomic<uint64_t> inv_epoch{0};
   // The launcher thread keeps one successor queued behind the running kernel
   // while requests come in, so a kernel that reaches its life limit hands
   // over to the next with no host call on any request's path (a launch call
@@ -507,9 +529,10 @@ void stop_and_drain(Server *s, const char *why) {
   }
   if (s->debug)
     fprintf(stderr,
-            "adl_bloom server %s: launched generation %u, started %u, done %u, alive %u (%s); "
-            "%s after %.1f us\n",
-            why, s->gen, started0, done0, alive0,
+            "adl_bloom server %s: clock calibration %s (samples folded %llu); launched generation %u, started %u, "
+            "done %u, alive %u (%s); %s after %.1f us\n",
+            why, g_clock.have.load() ? "set" : "unset", (unsigned long long)g_phases.stamped.load(),
+            s->gen, started0, done0, alive0,
             !s->launched ? "never launched"
             : started0 != s->gen ? "a successor queued, not started"
             : done0 != s->gen ? "running" : "exited",
@@ -673,6 +696,7 @@ Server *create() {
   s->idle_ticks = adl_host::knobs().server_idle_us * 100;
   s->life_ticks = adl_host::knobs().server_life_us * 100;
   s->debug = adl_host::knobs().debug;
+  s->invalidate_always = adl_host::knobs().server_invalidate;
   try {
     s->launcher = std::thread(launcher_main, s);
   } catch (...) {
@@ -725,7 +749,7 @@ uint32_t live_servers() {
 }
 
 int probe(Server *s, const uint8_t *h_keys, const uint64_t *h_offsets, uint32_t key_stride, uint64_t n,
-          const uint64_t *range, const uint8_t *kq, uint8_t *h_out) {
+          const uint64_t *range, const uint8_t *kq, uint64_t arena_epoch, uint8_t *h_out) {
   const uint64_t key_bytes = h_offsets ? h_offsets[n] - h_offsets[0] : n * (uint64_t)key_stride;
   if (!s || !eligible(n, key_bytes)) return ADL_ERR_INVALID_ARG;
   // a slot per thread and server (round-robin); threads beyond kSlots share
@@ -740,11 +764,14 @@ int probe(Server *s, const uint8_t *h_keys, const uint64_t *h_offsets, uint32_t 
   fold_phases(s->host, my, s->last_bell[my], s->last_seen[my]);
   // 31-bit sequence numbers, never 0 (the initial done); bit 31 of the bell
   // value says where the request is
-  s->seq[my] = (s->seq[my] + 1) & ~kInlineBit;
+  s->seq[my] = (s->seq[my] + 1) & kSeqMask;
   if (s->seq[my] == 0) s->seq[my] = 1;
   const bool inl = my < kInlineSlots && n == 1 && key_bytes <= kInlineKeyBytes && range[1] >= range[0] &&
                    range[1] - range[0] <= 0xFFFFFFFFull;
-  const uint32_t seq = s->seq[my] | (inl ? kInlineBit : 0u);
+  // the arena changed since the wave last invalidated its caches (or every
+  // request invalidates: ADL_BLOOM_SERVER_INVALIDATE=1, round 5's behaviour)
+  const bool inv = s->invalidate_always || arena_epoch > s->inv_epoch.load(std::memory_order_acquire);
+  const uint32_t seq = s->seq[my] | (inl ? kInlineBit : 0u) | (inv ? kInvalidateBit : 0u);
   s->last_bell[my] = seq;
   const auto tw0 = std::chrono::steady_clock::now();
   const uint8_t *kp = h_keys + (h_offsets ? h_offsets[0] : 0);
@@ -799,8 +826,19 @@ int probe(Server *s, const uint8_t *h_keys, const uint64_t *h_offsets, uint32_t 
   const auto t0 = std::chrono::steady_clock::now();
   auto since = [&] { return std::chrono::steady_clock::now() - t0; };
   uint32_t spins = 0;
+  // ADL_BLOOM_DEBUG: the longest stretch in which this thread did not run its
+  // spin loop (an interrupt, an SMI, a stalled core: time the operating
+  // system's switch counters do not see), to tell a host stall from an
+  // answer that reached host memory late
+  std::chrono::steady_clock::time_point tl = t0;
+  double max_gap_us = 0;
   while (!done) {
     if (answered(s, my, seq, &bits)) break;
+    if (s->debug) {
+      const auto tn = std::chrono::steady_clock::now();
+      max_gap_us = std::max(max_gap_us, std::chrono::duration<double, std::micro>(tn - tl).count());
+      tl = tn;
+    }
     __builtin_ia32_pause();
     if (++spins % 4096) continue;
     // unanswered for long (a kernel that failed, or one starved of its CU):
@@ -831,9 +869,10 @@ int probe(Server *s, const uint8_t *h_keys, const uint64_t *h_offsets, uint32_t 
       if (g_clock.get(&off))
         fprintf(stderr,
                 "adl_bloom server: slow request on the kernel's clock: the poll that found it started %.2f us after "
-                "the bell was written; the answer reached the host %.2f us later than the fastest answer does\n",
+                "the bell was written; the answer reached the host %.2f us later than the fastest answer does; "
+                "longest pause of this thread's answer wait: %.1f us\n",
                 (double)(int32_t)((uint32_t)w4 + off - host_tick(tb)) / 100.0,
-                (double)(int32_t)(host_tick(t1) - ((uint32_t)(w4 >> 32) + off)) / 100.0);
+                (double)(int32_t)(host_tick(t1) - ((uint32_t)(w4 >> 32) + off)) / 100.0, max_gap_us);
       fprintf(stderr,
               "adl_bloom server: slow request %.1f us (alive check / relaunch %.1f us%s, answer wait %.1f us; "
               "kernel%s: %.2f us since its previous poll; from the poll that found it: loads back %.2f, "
@@ -856,6 +895,11 @@ int probe(Server *s, const uint8_t *h_keys, const uint64_t *h_offsets, uint32_t 
     s->lcv.notify_one();
   }
   s->last_seen[my] = host_tick(std::chrono::steady_clock::now());
+  if (inv) {  // answered: the wave invalidated after every put up to arena_epoch
+    uint64_t e = s->inv_epoch.load(std::memory_order_relaxed);
+    while (e < arena_epoch && !s->inv_epoch.compare_exchange_weak(e, arena_epoch, std::memory_order_release)) {
+    }
+  }
   g_phases.requests.fetch_add(1, std::memory_order_relaxed);
   g_phases.host_ns.fetch_add(
       (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - tw0).count(),

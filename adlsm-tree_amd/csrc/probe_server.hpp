@@ -27,11 +27,13 @@ __attribute__((visibility("hidden"))) void destroy(Server *s);
 __attribute__((visibility("hidden"))) bool eligible(uint64_t n, uint64_t key_bytes);
 // n queries (keys by offsets or fixed stride), query q against the device
 // byte range [range[2q], range[2q+1]) of kq[q]-probe filter bits (each table's
-// block carries its own bits_per_key); answers to h_out.  Returns ADL_*
-// status, or kBusy when no answer came within kTimeout.
+// block carries its own bits_per_key); answers to h_out.  arena_epoch: the
+// caller's arena's put count, read after its ranges were resolved (the wave
+// invalidates its caches when it has not yet done so since that put).
+// Returns ADL_* status, or kBusy when no answer came within kTimeout.
 __attribute__((visibility("hidden"))) int probe(Server *s, const uint8_t *h_keys, const uint64_t *h_offsets,
                                                 uint32_t key_stride, uint64_t n, const uint64_t *range,
-                                                const uint8_t *kq, uint8_t *h_out);
+                                                const uint8_t *kq, uint64_t arena_epoch, uint8_t *h_out);
 
 // Servers that exist in this process (created, not destroyed).
 __attribute__((visibility("hidden"))) uint32_t live_servers();

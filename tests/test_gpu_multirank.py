@@ -176,3 +176,31 @@ def test_rccl_world1_collectives():
     assert res["reduce"] == [3.0, 0.25]
     assert res["routed_equal"] and res["scatter_equal"]
     assert res["served"] == 300_000
+
+
+def test_bench_line_two_ranks_one_gpu(tmp_path):
+    """bench.py's whole N > 1 default line -- the headline, compaction_strong,
+    headline_with_reader and the probe / varlen sub-records -- as two ranks on
+    cuda:0 over gloo (torch.distributed.run, 127.0.0.1): it runs to the end
+    and rank 0's JSON line carries every record with its parity, so the
+    driver's 8-GPU run of the same code has been exercised end to end."""
+    import subprocess
+    import sys
+
+    port = _free_port()
+    env = dict(os.environ, ADL_BENCH_BACKEND="gloo")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3",
+           "--warmup", "1", "--no-cpu-baseline", "--no-e2e"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=900, env=env, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    line = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(line) == 1, r.stdout[-2000:]
+    d = json.loads(line[0])
+    assert d["n_gpus"] == 2 and d["world"]["size"] == 2
+    assert d["parity"] == "bit-identical to reference (sha256)"
+    assert "MISMATCH" not in json.dumps(d)
+    assert d["compaction_strong"]["tables_per_gpu"] == 128
+    assert d["probe"]["parity"]["oracle"].startswith("all 100M answers bit-identical")
+    assert d["varlen"]["parity"] == "bit-identical to the oracle (sha256)"
+    assert d["headline_with_reader"]["parity"] == "bit-identical to reference (sha256)"

@@ -12,6 +12,9 @@
 #   TAILS=n         readpath_test --tails n (the server's phase stamps)
 #   PROF_PROBE=1    rocprofv3 kernel stats of bench.py --workload probe on
 #                   abl/base/libadlbloom.so and on the current library
+#   E2E_PARTS=1     tools/e2e_parts.py (a host-to-host build's parts)
+#   INV_AB=1        coexist with ADL_BLOOM_SERVER_INVALIDATE=1 (the server
+#                   invalidates its caches at every request, round 5) and 0
 #   DEBUG=1         the coexist runs with ADL_BLOOM_DEBUG=1 (slow Gets logged
 #                   with the server kernel's phase stamps)
 # Each GPU step has its own time limit; the first failure ends the script.
@@ -61,9 +64,18 @@ fi
 for v in ${COEXIST:-}; do
   ADL_BLOOM_DEBUG=${DEBUG:-0} ADL_BLOOM_BUILD_QUEUES=$v step coexist_q$v 300 adlsm-tree_amd/bin/readpath_test --coexist ${REPS:-20} || exit $?
 done
+if [ "${INV_AB:-0}" = 1 ]; then
+  for inv in 1 0; do
+    ADL_BLOOM_SERVER_INVALIDATE=$inv step coexist_inv$inv 300 adlsm-tree_amd/bin/readpath_test --coexist ${REPS:-20} \
+      || exit $?
+  done
+fi
 if [ -n "${PASSES:-}" ]; then
   ADL_BLOOM_BUILD_QUEUES=2 ADL_BLOOM_BUILD_QUEUE_PASSES=$PASSES step coexist_q2_p$PASSES 300 \
     adlsm-tree_amd/bin/readpath_test --coexist ${REPS:-20} || exit $?
+fi
+if [ "${E2E_PARTS:-0}" = 1 ]; then
+  step e2e_parts 300 python3 tools/e2e_parts.py || exit $?
 fi
 if [ -n "${TAILS:-}" ]; then
   step tails 300 adlsm-tree_amd/bin/readpath_test --tails $TAILS || exit $?
