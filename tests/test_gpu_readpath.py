@@ -341,9 +341,9 @@ def test_filter_cache_mixed_bpk(dev, ab, oracle, knobs):
     to the oracle with each block's own bits_per_key (the reference builds the
     BloomFilter of each block from its "bf:" info, src/filter_block.cpp:158-170;
     Level::Get reads every table of a level, src/revision.cpp:265-310)."""
-    bpks = [3, 10, 16, 3, 16, 10]
+    bpks = [3, 10, 16, 3, 16, 10, 0, 44]  # (0: a 7-byte bitmap, k = 1; 44: k = 30)
     tabs = [_varlen_block(oracle, 70 + t, 2500, b) for t, b in enumerate(bpks)]
-    cache = ab.FilterCache(16 << 20, max_tables=8)
+    cache = ab.FilterCache(16 << 20, max_tables=len(bpks))
     oids = [b"mix-%d" % t for t in range(len(bpks))]
     for o, (_, blk, _) in zip(oids, tabs):
         cache.put(o, blk)
