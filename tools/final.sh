@@ -3,16 +3,23 @@
 # integer issue) written into profiles/pmc_traffic.json first (bench.py reads
 # them), the GPU test suite, smoke(), the read-path latency bench, Gets beside
 # builds (readpath_test --coexist) and the server's tails, every bench
-# workload with CPU baselines, and rocprofv3 kernel traces of the headline and
-# var-len runs.
+# workload with CPU baselines, rocprofv3 kernel traces of the headline,
+# var-len and probe runs, and the driver's default bench line.
+# SKIP_PMC=1 / PMC_ONLY=1 split it over two calls (PMC_WORKLOADS= to narrow).
 set -u
 cd "$(dirname "$0")/.."
 OUT=gpurun_out/${TAG:?set TAG, e.g. TAG=r04a}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 step() { echo "=== $1 ($(date +%T))"; }
-step pmc
-bash tools/pmc_all.sh "$OUT/pmc" single varlen compaction probe > "$OUT/pmc.log" 2>&1 || { tail -5 "$OUT/pmc.log"; exit 1; }
+if [ "${SKIP_PMC:-0}" != 1 ]; then
+  step pmc
+  bash tools/pmc_all.sh "$OUT/pmc" ${PMC_WORKLOADS:-single varlen compaction probe} > "$OUT/pmc.log" 2>&1 || { tail -5 "$OUT/pmc.log"; exit 1; }
+  [ "${PMC_ONLY:-0}" = 1 ] && step bench_default
+timeout -k 10 600 python3 bench.py > "$OUT/bench_default.json" 2> "$OUT/bench_default.err" || exit 1
+tail -c 400 "$OUT/bench_default.json"
+exit 0
+fi
 step pytest
 timeout -k 10 900 python -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -n 4 "$OUT/pytest_gpu.log"; [ $rc -ne 0 ] && exit $rc
@@ -40,4 +47,7 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_varlen" -o run 
 step rocprof_probe
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_probe" -o run --output-format csv -- \
   python3 bench.py --steps 5 --warmup 2 --workload probe --no-cpu-baseline --no-e2e > "$OUT/prof_probe_bench.json" 2> "$OUT/prof_probe.err" || exit 1
+step bench_default
+timeout -k 10 600 python3 bench.py > "$OUT/bench_default.json" 2> "$OUT/bench_default.err" || exit 1
+tail -c 400 "$OUT/bench_default.json"
 exit 0
