@@ -35,9 +35,9 @@
 // The wave polls the bells and the inline lines, copies pending slots into LDS
 // four at a time (one load per lane per slot, one round trip for the group;
 // an inline request is copied from the lines already in LDS), hashes each query's
-// key from LDS (hash_bytes), tests its k bits in the arena with eight loads in
-// flight at once, and writes the answers with the sequence numbers.  The host
-// thread spins on its done line.
+// key from LDS (hash_lds: 8-byte LDS reads and alignbyte), tests its k bits in
+// the arena with six loads in flight at once, and writes the answers with the
+// sequence numbers.  The host thread spins on its done line.
 //
 // Lifetime.  The kernel leaves when it has been idle for idle_ticks, when it
 // has run for life_ticks, or when the host raises ctl->stop (cache teardown),
@@ -177,45 +177,57 @@ struct Prep {
   uint32_t k, mbits, h1, h2;
 };
 
-__device__ __forceinline__ Prep prep_query(uint32_t k, uint64_t b0, uint64_t b1, const uint8_t *key, uint32_t klen) {
+// The key is at byte `off` of the LDS words `stage` (8-byte aligned, 8 bytes
+// of slack after the key): hash_lds reads it with ds_read_b64 + alignbyte
+// (round 5 hashed it through a byte pointer: four LDS byte reads per word).
+__device__ __forceinline__ Prep prep_query(uint32_t k, uint64_t b0, uint64_t b1, const uint32_t *stage, uint32_t off,
+                                           uint32_t klen) {
   Prep p{b0, min(k, 30u), 0u, 0u, 0u};
   // 0 for an empty range or a filter of 2^31 bits or more (src/filter_block.cpp:50)
   p.mbits = b1 > b0 && b1 - b0 <= 0x0fffffffull ? (uint32_t)((b1 - b0) * 8) : 0u;
-  if (p.mbits) hash_bytes(key, klen, kSeed1, kSeed2, p.h1, p.h2);
+  if (p.mbits) hash_lds(stage, off, klen, p.h1, p.h2);
   return p;
 }
 
-// 1 iff all k bits are set (0 for an empty range)
+// 1 iff all k bits are set (0 for an empty range).  Six reads in flight: k
+// of the default bits_per_key (10) in one round, and five fewer VGPRs spilled
+// than with eight (profiles/r06/server/reads_in_flight_8_vs_6.txt: the same
+// latency within noise)
+constexpr uint32_t kReads = 6;
 __device__ __forceinline__ uint32_t read_bits(const Prep &p) {
   if (!p.mbits) return 0;
   const FastMod mod = fastmod_for(p.mbits);
   const uint8_t *bm = reinterpret_cast<const uint8_t *>(p.b0);
   // the answer is the AND of the k bits (src/filter_block.cpp:54-59; the
-  // early exit changes no answer): 8 reads in flight at a time
+  // early exit changes no answer): kReads reads in flight at a time
   uint32_t all = 1;
-  for (uint32_t g = 0; g < p.k; g += 8) {
-    uint32_t w[8];
+  for (uint32_t g = 0; g < p.k; g += kReads) {
+    uint32_t w[kReads];
 #pragma unroll
-    for (uint32_t u = 0; u < 8; ++u) {
+    for (uint32_t u = 0; u < kReads; ++u) {
       const uint32_t q = fastmod(p.h1 + (g + u < p.k ? g + u : 0u) * p.h2, mod);  // past k: bit 0 again
       w[u] = (uint32_t)(bm[q >> 3] >> (q & 7));
     }
 #pragma unroll
-    for (uint32_t u = 0; u < 8; ++u) all &= w[u];
+    for (uint32_t u = 0; u < kReads; ++u) all &= w[u];
   }
   return all & 1u;
 }
 
-// Query q of a slot staged in LDS.
+// Query q of a slot staged in LDS (the slot's keys end 16 bytes before it does).
 __device__ __forceinline__ Prep prep_slot_query(const Slot &sl, uint32_t q) {
   const uint32_t ko = min((uint32_t)sl.koff[q], adl_srv::kMaxKeyBytes);
   const uint32_t ke = min(max((uint32_t)sl.koff[q + 1], ko), adl_srv::kMaxKeyBytes);
-  return prep_query(sl.kq[q], sl.range[2 * q], sl.range[2 * q + 1], sl.keys + ko, ke - ko);
+  return prep_query(sl.kq[q], sl.range[2 * q], sl.range[2 * q + 1], reinterpret_cast<const uint32_t *>(&sl),
+                    kKeyOff + ko, ke - ko);
 }
 
-// The request of a line staged in LDS.
-__device__ __forceinline__ Prep prep_line(const Line &ln) {
-  return prep_query(ln.k_klen & 0xFFu, ln.begin, ln.begin + ln.len, ln.key, min(ln.k_klen >> 8, kInlineKeyBytes));
+// The request of line i staged in LDS (lines: the LDS copy of all of them,
+// with slack words after the last).
+__device__ __forceinline__ Prep prep_line(const uint32_t *lines, uint32_t i) {
+  const Line &ln = *reinterpret_cast<const Line *>(lines + 16 * i);
+  return prep_query(ln.k_klen & 0xFFu, ln.begin, ln.begin + ln.len, lines, 64u * i + (uint32_t)offsetof(Line, key),
+                    min(ln.k_klen >> 8, kInlineKeyBytes));
 }
 
 // One wave.  Lane l polls bell l.  Pending slots are staged kGroup at a time
@@ -226,7 +238,7 @@ __device__ __forceinline__ Prep prep_line(const Line &ln) {
 // kLdsReserveWords): a Get does not wait for a build.  amdgpu_num_vgpr(16) is
 // doubled for gfx950's unified register file (as kPassARegs' 60 -> 120): the
 // code object's .vgpr_count is 32.  Unconstrained the kernel would take 63, so
-// 19 VGPRs spill to scratch (76 B per lane, with the phase stamps): kernel arguments and loop state,
+// 13 VGPRs spill to scratch (52 B per lane, with the phase stamps): kernel arguments and loop state,
 // reloaded once per poll and once per served group, from the L1/L2 the wave
 // alone uses.  tools/kernel_resources.py prints both from the built library
 // and tests/test_kernel_resources.py pins them (no other product kernel on the
@@ -234,7 +246,7 @@ __device__ __forceinline__ Prep prep_line(const Line &ln) {
 __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(16))) void probe_server_kernel(
     Area *area, uint64_t idle_ticks, uint64_t life_ticks, uint32_t gen) {
   __shared__ __attribute__((aligned(16))) uint8_t lslot[kGroup][kSlotBytes];
-  __shared__ __attribute__((aligned(16))) uint32_t lline[kInlineSlots * 16];  // the lines of the last poll
+  __shared__ __attribute__((aligned(16))) uint32_t lline[kInlineSlots * 16 + 4];  // the lines of the last poll (+ hash_lds slack)
   const uint32_t lane = threadIdx.x;
   // a successor queued behind a running kernel (Server::launcher) announces
   // itself: alive again, and its generation started
@@ -330,7 +342,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(16))) void probe
       Prep pr{0ull, 0u, 0u, 0u, 0u};
       const uint32_t bj = (uint32_t)__shfl((int)bell, (int)(j < kSlots ? j : 0u));
       if (j < kSlots && (bj & kInlineBit)) {
-        if (q == 0) pr = prep_line(*reinterpret_cast<const Line *>(&lline[16 * (j & (kInlineSlots - 1))]));
+        if (q == 0) pr = prep_line(lline, j & (kInlineSlots - 1));
       } else if (j < kSlots) {
         const Slot &sl = *reinterpret_cast<const Slot *>(lslot[u]);
         if (q < min(sl.n, adl_srv::kMaxQ)) pr = prep_slot_query(sl, q);
