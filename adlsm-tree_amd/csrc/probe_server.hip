@@ -326,7 +326,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(16))) void probe
         js[u] = m ? (uint32_t)__builtin_ctzll(m) : kSlots;
         m &= m - 1;  // (m = 0 stays 0)
         // (an inline request's slot is not read: its line is in LDS)
-        const uint32_t bj = (uint32_t)__shfl((int)bell, (int)(js[u] < kSlots ? js[u] : 0u));
+        // (js[u] is wave-uniform: a v_readlane, not an LDS permute round trip)
+        const uint32_t bj = __builtin_amdgcn_readlane(bell, js[u] < kSlots ? js[u] : 0u);
         const uint64_t *src = reinterpret_cast<const uint64_t *>(&area->slot[js[u] < kSlots ? js[u] : 0]);
         v[u] = js[u] < kSlots && !(bj & kInlineBit) ? __hip_atomic_load(src + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
                                                      : 0ull;
