@@ -67,7 +67,10 @@ constexpr uint32_t kChunkEst = 5500;      // keys per pass-A chunk (k = 6), for 
 constexpr uint32_t kClaimTiles = 10;      // claim layout by default only up to this many tiles per filter
 constexpr uint32_t kClaimSlack = 125;     // claim layout: region = k*C positions * 125 %
 constexpr uint32_t kClaimSigma = 4;       // ... kept when a tile's share clears its mean run by 4 sigma
-constexpr uint32_t kHvKeys = 512;         // keys per hash_var_kernel run
+#ifndef ADL_HV_KEYS
+#define ADL_HV_KEYS 512
+#endif
+constexpr uint32_t kHvKeys = ADL_HV_KEYS;  // keys per hash_var_kernel run
 constexpr uint32_t kBlockA = 1024;        // pass A threads per workgroup (one workgroup per CU)
 constexpr uint32_t kDdLog2Max = 11;       // log2 slots of pass A's repeated-hash table, at most
 // LDS pass A leaves free on its CU (3 KiB): the resident probe server's
@@ -585,7 +588,10 @@ __global__ __launch_bounds__(BLOCK) kPassARegs void bloom_bin_kernel(BuildArgs a
 // Measured against hashing in sorted order straight from global memory (lanes
 // reading scattered keys): L2 missed each key line ~3.7 times, 1.4 GB fetched
 // for 0.4 GB of keys.
-constexpr int kHvBlock = 256;
+#ifndef ADL_HV_BLOCK
+#define ADL_HV_BLOCK 256
+#endif
+constexpr int kHvBlock = ADL_HV_BLOCK;
 constexpr uint32_t kHvBins = 512;          // exact key length 0..510; 511 = longer
 // LDS staging of a run's key bytes: 48 bytes per key (mean key ~40 B)
 template <uint32_t S>

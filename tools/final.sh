@@ -15,10 +15,12 @@ step() { echo "=== $1 ($(date +%T))"; }
 if [ "${SKIP_PMC:-0}" != 1 ]; then
   step pmc
   bash tools/pmc_all.sh "$OUT/pmc" ${PMC_WORKLOADS:-single varlen compaction probe} > "$OUT/pmc.log" 2>&1 || { tail -5 "$OUT/pmc.log"; exit 1; }
-  [ "${PMC_ONLY:-0}" = 1 ] && step bench_default
-timeout -k 10 600 python3 bench.py > "$OUT/bench_default.json" 2> "$OUT/bench_default.err" || exit 1
-tail -c 400 "$OUT/bench_default.json"
-exit 0
+  if [ "${PMC_ONLY:-0}" = 1 ]; then
+    step bench_default
+    timeout -k 10 600 python3 bench.py > "$OUT/bench_default.json" 2> "$OUT/bench_default.err" || exit 1
+    tail -c 400 "$OUT/bench_default.json"
+    exit 0
+  fi
 fi
 step pytest
 timeout -k 10 900 python -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1
