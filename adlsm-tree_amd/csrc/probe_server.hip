@@ -425,8 +425,10 @@ struct Server {
   bool debug = false;  // ADL_BLOOM_DEBUG at creation (the launcher thread must not read knobs() while a reload runs)
   bool invalidate_always = false;  // ADL_BLOOM_SERVER_INVALIDATE=1 at creation
   // the cache arena's epoch (bumped by each published put) up to which the
-  // running wave has invalidated its caches; a new kernel starts with clean
-  // caches, so a launch counts too (ensure_running)
+  // server's waves have invalidated their caches: raised by a request that
+  // carried kInvalidateBit once it is answered.  A launch does not raise it
+  // (a fresh wave reads through the same L2, which may hold lines cached
+  // before the put).
   std::atomic<uint64_t> inv_epoch{0};
   // The launcher thread keeps one successor queued behind the running kernel
   // while requests come in, so a kernel that reaches its life limit hands
@@ -461,12 +463,16 @@ PhaseStats g_phases;
 struct ClockCal {
   std::atomic<uint32_t> ref{0};
   std::atomic<int32_t> best{INT32_MAX};
-  std::atomic<bool> have{false};
+  std::atomic<bool> init{false}, have{false};  // init: a thread is setting ref; have: ref is set
   void sample(uint32_t host_tick, uint32_t gpu_tick) {
     const uint32_t d = host_tick - gpu_tick;
-    bool expect = false;
-    if (!have.load(std::memory_order_acquire) && have.compare_exchange_strong(expect, true)) ref.store(d);
-    const int32_t rel = (int32_t)(d - ref.load());
+    if (!have.load(std::memory_order_acquire)) {
+      bool expect = false;
+      if (!init.compare_exchange_strong(expect, true)) return;  // another thread sets ref: skip this sample
+      ref.store(d, std::memory_order_relaxed);
+      have.store(true, std::memory_order_release);
+    }
+    const int32_t rel = (int32_t)(d - ref.load(std::memory_order_relaxed));
     int32_t cur = best.load(std::memory_order_relaxed);
     while (rel < cur && !best.compare_exchange_weak(cur, rel)) {
     }
